@@ -1,0 +1,25 @@
+# Builds the C-ABI library nerf_pl_amd/libnerf_pl_amd.so for gfx950 (MI355X)
+# and the C pieces of the oracle.  `make -j8`
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+SRC := $(wildcard nerf_pl_amd/csrc/*.hip)
+HDR := $(wildcard nerf_pl_amd/csrc/*.h)
+OBJ := $(patsubst nerf_pl_amd/csrc/%.hip,build/%.o,$(SRC))
+LIB := nerf_pl_amd/libnerf_pl_amd.so
+
+all: $(LIB)
+
+build/%.o: nerf_pl_amd/csrc/%.hip $(HDR) | build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+build:
+	mkdir -p build
+
+$(LIB): $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean

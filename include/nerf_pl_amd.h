@@ -1,0 +1,113 @@
+/* nerf_pl_amd -- C ABI of the MI355X (gfx950) volumetric-rendering hot path.
+ *
+ * Drop-in boundary for ktiwary2/nerf_pl's render_rays / sample_pdf / NeRF
+ * path (models/rendering.py, models/nerf.py).  The reference is pure Python on
+ * PyTorch; its only native dependency is the torchsearchsorted extension
+ * (.gitmodules:1-3), which nr_sample_pdf replaces.  Each entry point below
+ * names the reference code it stands in for.
+ *
+ * Conventions
+ *   - every pointer is device memory allocated by the caller (float32, rows
+ *     contiguous); the library never allocates, frees or retains pointers;
+ *   - `stream` is a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ *     work is enqueued asynchronously and no call synchronises the host;
+ *   - return 0 on success, a hipError_t or NR_EINVAL (10001) / NR_EALIGN (10002)
+ *     otherwise; nr_last_error() gives a thread-local message;
+ *   - "rays" are (n_rays, 8) = [origin(3), direction(3), near, far]
+ *     (rendering.py:209-210); per-sample arrays are ray-major (ray*S + k).
+ *   - random draws: a non-NULL replay array is used verbatim (parity with the
+ *     reference's torch.rand / torch.randn); NULL means draw in-kernel from
+ *     Philox4x32-10 keyed by (seed, stream id, element index).
+ */
+#ifndef NERF_PL_AMD_H
+#define NERF_PL_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Thread-local text of the last error. */
+const char* nr_last_error(void);
+
+/* Layout constants shared with the Python packer (0: forward packed floats,
+ * 1: head offset, 2: backward packed floats, 3: saved floats/sample,
+ * 4: gradient floats/sample, 5: head floats, 6..8: layer offsets). */
+int64_t nr_layout_query(int what);
+
+/* Gather the flat parameter buffer (595,844 floats, NeRF.named_parameters()
+ * order) into MFMA fragment order: out[i] = map[i] >= 0 ? flat[map[i]] : 0.
+ * Replaces nothing in the reference (its GEMMs read nn.Linear weights
+ * directly, nerf.py:60-81); run once per weight update. */
+int nr_pack(const float* flat, const int32_t* map, int64_t n, float* out, void* stream);
+
+/* Embedding.forward (models/nerf.py:21-38): x (n,3) -> out (n, 3*(2*n_freqs+1)). */
+int nr_embed(const float* x, int64_t n, int n_freqs, float* out, void* stream);
+
+/* Fused positional encoding + NeRF MLP forward -- replaces the chunked
+ * `embedding_xyz` + `NeRF.forward` loop of inference() (rendering.py:141-161,
+ * nerf.py:83-124).
+ *   Ray path (x == NULL): sample s uses point o + d*z[s] of ray s/samples_per_ray
+ *     (rendering.py:234-235) and that ray's direction encoding.
+ *   Embedded path (x != NULL): x is (n, xstride) pre-embedded [xyz_emb(63),
+ *     dir_emb(27)] or xyz_emb only when sigma_only (NeRF.forward(x) API).
+ *   out: (n,4) [rgb, sigma] or (n,1) sigma when sigma_only.
+ *   save: NULL for inference, else n*nr_layout_query(3) floats of activations
+ *     kept for nr_mlp_bwd / nr_wgrad (training). */
+int nr_mlp_fwd(const float* packed_fwd, const float* rays, const float* z, int64_t n,
+               int samples_per_ray, const float* x, int xstride, int sigma_only, float* out,
+               float* save, void* stream);
+
+/* MLP backward, data-gradient chain (autograd of nerf.py:83-124): from
+ * g_out (n,4) = d[rgb, sigma] writes every layer's pre-activation gradient to
+ * grad_ws (n*nr_layout_query(4) floats). */
+int nr_mlp_bwd(const float* packed_bwd, const float* packed_fwd, const float* out,
+               const float* g_out, const float* save, int64_t n, float* grad_ws, void* stream);
+
+/* MLP backward, weight gradients: sum over all n samples of dz^T x for every
+ * layer (split over workgroups, reduced in a fixed order), written as
+ * d(loss)/d(params) into grad_flat (595,844 floats, named_parameters order). */
+int64_t nr_wgrad_workspace_bytes(int64_t n);
+int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
+             float* grad_flat, void* stream);
+
+/* Stratified coarse depths (rendering.py:216-232).  tlin = torch.linspace(0,1,S)
+ * values; u: (n_rays,S) replay of torch.rand or NULL. */
+int nr_coarse_z(const float* rays, const float* tlin, int64_t n_rays, int n_samples,
+                int use_disp, float perturb, const float* u, uint64_t seed, float* z_out,
+                void* stream);
+
+/* Volume compositing (rendering.py:169-198), one wave per ray.  raw rows of
+ * raw_stride floats with rgb at 0..2 and sigma at sig_col.  noise: (n_rays,S)
+ * replay of torch.randn or NULL.  Writes weights (n_rays,S), opacity, and unless
+ * weights_only rgb (n_rays,3) and depth. */
+int nr_composite_fwd(const float* raw, int raw_stride, int sig_col, const float* z,
+                     const float* rays, const float* noise, float noise_std, uint64_t seed,
+                     int rng_stream, int64_t n_rays, int n_samples, int white_back,
+                     int weights_only, float* rgb, float* depth, float* opacity,
+                     float* weights, void* stream);
+
+/* Autograd of the compositing step: d(rgb, depth, opacity) -> g_raw (n_rays*S, 4)
+ * = d[rgb_i, sigma_i].  Any gradient pointer may be NULL (zero). */
+int nr_composite_bwd(const float* raw, const float* z, const float* rays, const float* noise,
+                     float noise_std, uint64_t seed, int rng_stream, int64_t n_rays,
+                     int n_samples, int white_back, const float* g_rgb, const float* g_depth,
+                     const float* g_opacity, float* g_raw, void* stream);
+
+/* sample_pdf (rendering.py:14-48) replacing torchsearchsorted.searchsorted
+ * (side='right', rendering.py:37), fused with sort(cat[z_coarse, z_pdf])
+ * (rendering.py:257).  weights: coarse weights (n_rays, n_samples), bins are
+ * columns 1..n_samples-2.  u, jitter: (n_rays, n_importance) replays or NULL.
+ * z_pdf (n_rays, n_importance) and/or z_fine (n_rays, n_samples+n_importance). */
+int nr_sample_pdf(const float* weights, int n_samples, const float* rays,
+                  const float* z_coarse, const float* u, const float* jitter, uint64_t seed,
+                  int64_t n_rays, int n_importance, float* z_pdf, float* z_fine, void* stream);
+
+/* Test hook: one v_mfma_f32_32x32x2_f32 on A (32x2), B (2x32) -> D (32x32). */
+int nr_probe_mfma32(const float* a, const float* b, float* d, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NERF_PL_AMD_H */

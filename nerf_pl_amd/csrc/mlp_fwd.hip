@@ -1,0 +1,298 @@
+// Fused positional-encoding + NeRF MLP forward (models/nerf.py:21-38, 83-124;
+// the chunked MLP loop of models/rendering.py:141-161).
+//
+// One wave evaluates 32 samples through all layers.  Every layer is computed in
+// transposed form D[feature][sample] on v_mfma_f32_32x32x2_f32 so the
+// accumulators (feature in registers, sample on the lane) are directly the B
+// operand of the next layer: activations never leave registers.  Weights are
+// pre-packed in MFMA A-fragment order (packing.py) and streamed from L2/HBM as
+// one coalesced 1 KiB float4 wave load per (4 k-steps x 32 rows), prefetched
+// one group ahead.  sin/cos positional encodings are computed in registers
+// and fed straight into the first layer and the skip layer.
+#include "layout.h"
+
+namespace {
+
+constexpr int kWaves = 4;   // waves per workgroup (one per SIMD)
+
+template <int NT>
+__device__ __forceinline__ void ld_wgrp(const float* __restrict__ w, int grp, int lane,
+                                        f32x4 (&dst)[NT]) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(w) + (size_t)grp * NT * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) dst[t] = p[t * 64];
+}
+
+// acc[t] += sum_g Wpacked[g][t] * B(g), g in [0, KS).  getb(g) must fold to a
+// register for compile-time g.
+template <int KS, int NT, typename GetB>
+__device__ __forceinline__ void mm_acc(const float* __restrict__ w, int lane, f32x16 (&acc)[NT],
+                                       GetB getb) {
+    static_assert(KS % 8 == 0, "k-steps must be a multiple of 8");
+    f32x4 wa[NT], wb[NT];
+    ld_wgrp<NT>(w, 0, lane, wa);
+#pragma unroll
+    for (int grp = 0; grp < KS / 4; grp += 2) {
+        ld_wgrp<NT>(w, grp + 1, lane, wb);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const float b = getb(grp * 4 + kk);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wa[t][kk], b, acc[t]);
+        }
+        if (grp + 2 < KS / 4) ld_wgrp<NT>(w, grp + 2, lane, wa);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const float b = getb(grp * 4 + 4 + kk);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wb[t][kk], b, acc[t]);
+        }
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void init_bias(f32x16 (&acc)[NT], const float* __restrict__ b, int h) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(b + 32 * t + 8 * q + 4 * h);
+            acc[t][4 * q + 0] = v[0];
+            acc[t][4 * q + 1] = v[1];
+            acc[t][4 * q + 2] = v[2];
+            acc[t][4 * q + 3] = v[3];
+        }
+}
+
+template <int NT>
+__device__ __forceinline__ void relu(f32x16 (&acc)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] > 0.f ? acc[t][r] : 0.f;
+}
+
+// store the accumulator rows of one sample: row = dst + sample*width, feature
+// 32t + 8q + 4h + e lives in register 4q+e of tile t.
+template <int NT>
+__device__ __forceinline__ void store_rows(const f32x16 (&acc)[NT], float* __restrict__ row, int h) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            f32x4 v = {acc[t][4 * q + 0], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+            *reinterpret_cast<f32x4*>(row + 32 * t + 8 * q + 4 * h) = v;
+        }
+}
+
+// <w, acc> over this lane's features, then summed over both lane halves.
+template <int NT>
+__device__ __forceinline__ float head_dot(const f32x16 (&acc)[NT], const float* __restrict__ w, int h) {
+    float p = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(w + 32 * t + 8 * q + 4 * h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) p = fmaf(acc[t][4 * q + e], v[e], p);
+        }
+    return p + __shfl_xor(p, 32);
+}
+
+// Positional encoding of one point, in packed k order (packing.py pe_feature):
+// g=0 (x|y), g=1 (z|pad), g=2..1+NP sin pairs, g=2+NP..1+2NP cos pairs.
+// Lane half h evaluates pair member m = i + NP*h: sin/cos(2^(m/3) * p[m%3]).
+template <int NP, int KS>
+__device__ __forceinline__ void pe_encode(float (&pe)[KS], float px, float py, float pz, int h) {
+    pe[0] = h ? py : px;
+    pe[1] = h ? 0.f : pz;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int m = i + NP * h;
+        const int k = (m * 11) >> 5;     // m / 3 for m < 32
+        const int c = m - 3 * k;
+        const float v = c == 0 ? px : (c == 1 ? py : pz);
+        const float arg = v * (float)(1 << k);   // freq * x, freq = 2^k exactly (nerf.py:17,36)
+        float s, co;
+        sincosf(arg, &s, &co);
+        pe[2 + i] = s;
+        pe[2 + NP + i] = co;
+    }
+#pragma unroll
+    for (int g = 2 + 2 * NP; g < KS; ++g) pe[g] = 0.f;
+}
+
+// Same channels gathered from a pre-embedded row (NeRF.forward(x) API path).
+template <int NP, int KS>
+__device__ __forceinline__ void pe_gather(float (&pe)[KS], const float* __restrict__ row, int h) {
+    pe[0] = row[h];
+    pe[1] = h ? 0.f : row[2];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int m = i + NP * h;
+        const int k = (m * 11) >> 5;
+        const int c = m - 3 * k;
+        pe[2 + i] = row[3 + 6 * k + c];
+        pe[2 + NP + i] = row[6 + 6 * k + c];
+    }
+#pragma unroll
+    for (int g = 2 + 2 * NP; g < KS; ++g) pe[g] = 0.f;
+}
+
+struct FwdArgs {
+    const float* packed;
+    const float* rays;   // (n_rays, 8) [o, d, near, far]
+    const float* z;      // (n) depths, sample-major (ray*spr + k)
+    const float* x;      // (n, xstride) embedded input (EMB path)
+    int n;               // samples
+    int spr;             // samples per ray
+    int xstride;
+    float* out;          // (n, 4) [rgb, sigma] or (n, 1) sigma
+    float* save;         // saved activations (training) or nullptr
+};
+
+template <bool EMB, bool SIGMA_ONLY>
+__global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int h = lane >> 5;
+    const int s_raw = (blockIdx.x * kWaves + wave) * 32 + (lane & 31);
+    const bool valid = s_raw < a.n;
+    const int s = valid ? s_raw : a.n - 1;
+    const float* P = a.packed;
+    const float* H = a.packed + NR_F_HEAD;
+    const bool save = a.save != nullptr;
+    NrSave sv(a.save, a.n);
+
+    // ---- point and direction ------------------------------------------------
+    float px, py, pz, dx = 0.f, dy = 0.f, dz = 0.f;
+    const float* xrow = nullptr;
+    if constexpr (EMB) {
+        xrow = a.x + (size_t)s * a.xstride;
+        px = py = pz = 0.f;
+    } else {
+        const int ray = s / a.spr;
+        const float* r = a.rays + (size_t)ray * 8;
+        const float zz = a.z[s];
+        // rendering.py:234 -- o + d*z as separate fp32 mul and add
+        px = nr_add(r[0], nr_mul(r[3], zz));
+        py = nr_add(r[1], nr_mul(r[4], zz));
+        pz = nr_add(r[2], nr_mul(r[5], zz));
+        dx = r[3]; dy = r[4]; dz = r[5];
+    }
+
+    f32x16 A[8], B[8];
+    {   // layer 1: PE(63) -> 256
+        float pe[NR_PE_KSTEPS];
+        if constexpr (EMB) pe_gather<15, NR_PE_KSTEPS>(pe, xrow, h);
+        else pe_encode<15, NR_PE_KSTEPS>(pe, px, py, pz, h);
+        if (save && valid) {
+            float* row = sv.pe + (size_t)s * NR_SAVE_PE;
+#pragma unroll
+            for (int g = 0; g < NR_PE_KSTEPS; ++g) row[2 * g + h] = pe[g];
+        }
+        init_bias<8>(A, H + NR_H_BIAS(1), h);
+        mm_acc<NR_PE_KSTEPS, 8>(P + NR_F_L1, lane, A, [&](int g) { return pe[g]; });
+        relu<8>(A);
+    }
+    if (save && valid) store_rows<8>(A, sv.h[0] + (size_t)s * 256, h);
+
+#define NR_DENSE(DST, SRC, LOFF, L)                                                   \
+    init_bias<8>(DST, H + NR_H_BIAS(L), h);                                            \
+    mm_acc<128, 8>(P + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; });   \
+    relu<8>(DST);                                                                      \
+    if (save && valid) store_rows<8>(DST, sv.h[L - 1] + (size_t)s * 256, h);
+
+    NR_DENSE(B, A, NR_F_L2, 2)
+    NR_DENSE(A, B, NR_F_L3, 3)
+    NR_DENSE(B, A, NR_F_L4, 4)
+    {   // layer 5: cat[PE, h4] -> 256 (skip, nerf.py:108-109); PE recomputed
+        float pe[NR_PE_KSTEPS];
+        if constexpr (EMB) pe_gather<15, NR_PE_KSTEPS>(pe, xrow, h);
+        else pe_encode<15, NR_PE_KSTEPS>(pe, px, py, pz, h);
+        init_bias<8>(A, H + NR_H_BIAS(5), h);
+        mm_acc<NR_PE_KSTEPS, 8>(P + NR_F_L5, lane, A, [&](int g) { return pe[g]; });
+        mm_acc<128, 8>(P + NR_F_L5 + NR_PL(NR_PE_KSTEPS, 8), lane, A,
+                       [&](int g) { return B[g >> 4][g & 15]; });
+        relu<8>(A);
+        if (save && valid) store_rows<8>(A, sv.h[4] + (size_t)s * 256, h);
+    }
+    NR_DENSE(B, A, NR_F_L6, 6)
+    NR_DENSE(A, B, NR_F_L7, 7)
+    NR_DENSE(B, A, NR_F_L8, 8)
+#undef NR_DENSE
+
+    // sigma = Linear(256, 1)(h8), raw (nerf.py:112)
+    const float sigma = head_dot<8>(B, H + NR_H_WSIG, h) + H[NR_H_BSIG];
+    if constexpr (SIGMA_ONLY) {
+        if (valid && h == 0) a.out[s] = sigma;
+        return;
+    } else {
+        // xyz_encoding_final: Linear(256,256), no activation (nerf.py:116)
+        init_bias<8>(A, H + NR_H_BFINAL, h);
+        mm_acc<128, 8>(P + NR_F_FINAL, lane, A, [&](int g) { return B[g >> 4][g & 15]; });
+        if (save && valid) store_rows<8>(A, sv.feat + (size_t)s * 256, h);
+
+        // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
+        float dpe[NR_DIR_KSTEPS];
+        if constexpr (EMB) pe_gather<6, NR_DIR_KSTEPS>(dpe, xrow + NR_XYZ_CH, h);
+        else pe_encode<6, NR_DIR_KSTEPS>(dpe, dx, dy, dz, h);
+        if (save && valid) {
+            float* row = sv.dirpe + (size_t)s * NR_SAVE_DIR;
+#pragma unroll
+            for (int g = 0; g < NR_DIR_KSTEPS; ++g) row[2 * g + h] = dpe[g];
+        }
+        f32x16 C[4];
+        init_bias<4>(C, H + NR_H_BDIR, h);
+        mm_acc<128, 4>(P + NR_F_DIR, lane, C, [&](int g) { return A[g >> 4][g & 15]; });
+        mm_acc<NR_DIR_KSTEPS, 4>(P + NR_F_DIR + NR_PL(128, 4), lane, C,
+                                 [&](int g) { return dpe[g]; });
+        relu<4>(C);
+        if (save && valid) store_rows<4>(C, sv.hdir + (size_t)s * 128, h);
+
+        // rgb = Sigmoid(Linear(128,3)) (nerf.py:79-81,120)
+        float rgb[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float zc = head_dot<4>(C, H + NR_H_WRGB + 128 * c, h) + H[NR_H_BRGB + c];
+            rgb[c] = 1.f / (1.f + expf(-zc));
+        }
+        if (valid && h == 0) {
+            f32x4 o = {rgb[0], rgb[1], rgb[2], sigma};
+            *reinterpret_cast<f32x4*>(a.out + (size_t)s * 4) = o;
+        }
+    }
+}
+
+}  // namespace
+
+NR_API int nr_mlp_fwd(const float* packed, const float* rays, const float* z, int64_t n,
+                      int samples_per_ray, const float* x, int xstride, int sigma_only,
+                      float* out, float* save, void* stream) {
+    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_fwd: n=%lld out of range", (long long)n);
+    if (n == 0) return 0;
+    NR_REQUIRE(packed && out, "nr_mlp_fwd: null packed/out");
+    NR_REQUIRE(((uintptr_t)packed & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                   ((uintptr_t)save & 15) == 0,
+               "nr_mlp_fwd: packed/out/save must be 16-byte aligned");
+    const bool emb = x != nullptr;
+    if (emb) {
+        NR_REQUIRE(xstride >= (sigma_only ? NR_XYZ_CH : NR_XYZ_CH + NR_DIR_CH),
+                   "nr_mlp_fwd: xstride %d too small", xstride);
+    } else {
+        NR_REQUIRE(rays && z && samples_per_ray > 0, "nr_mlp_fwd: rays/z/samples_per_ray");
+    }
+    FwdArgs a{packed, rays, z, x, (int)n, samples_per_ray, xstride, out, save};
+    const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
+    hipStream_t st = (hipStream_t)stream;
+    if (emb) {
+        if (sigma_only) mlp_fwd_kernel<true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_fwd_kernel<true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+    } else {
+        if (sigma_only) mlp_fwd_kernel<false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_fwd_kernel<false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+    }
+    NR_LAUNCH_CHECK("nr_mlp_fwd");
+    return 0;
+}

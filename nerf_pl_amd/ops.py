@@ -1,0 +1,161 @@
+"""Tensor-level wrappers over the C ABI (one function per entry point).
+
+All tensors must be float32, contiguous and on the same HIP device; kernels are
+enqueued on the current torch stream.  No CPU path exists: non-device tensors
+raise.
+"""
+from __future__ import annotations
+
+import functools
+
+import numpy as np
+import torch
+
+from . import packing
+from ._lib import call, lib, ptr, stream_of
+
+SAVE_PER_SAMPLE = 64 + 8 * 256 + 256 + 128 + 32        # csrc/layout.h NR_SAVE_PER_SAMPLE
+GRAD_PER_SAMPLE = 8 * 256 + 256 + 128 + 4              # NR_GRAD_PER_SAMPLE
+FWD_PACKED = packing.layer_offsets(packing.FWD_LAYERS)[1] + packing.HEAD_SIZE
+BWD_PACKED = packing.layer_offsets(packing.BWD_LAYERS)[1]
+
+
+def _dev(t: torch.Tensor, name: str, shape_last=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"nerf_pl_amd: {name} must live on a HIP device (got {t.device}); "
+                           "this package has no CPU path")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+    if not t.is_contiguous():
+        t = t.contiguous()
+    if shape_last is not None and t.shape[-1] != shape_last:
+        raise ValueError(f"{name}: last dim must be {shape_last}, got {tuple(t.shape)}")
+    return t
+
+
+@functools.lru_cache(maxsize=None)
+def _maps(device_index: int):
+    dev = torch.device("cuda", device_index)
+    fwd = torch.from_numpy(packing.build_fwd_map()).to(dev)
+    bwd = torch.from_numpy(packing.build_bwd_map()).to(dev)
+    return fwd, bwd
+
+
+@functools.lru_cache(maxsize=None)
+def linspace_table(n: int, device_index: int) -> torch.Tensor:
+    # torch.linspace on the CPU -- the exact values the reference uses (rendering.py:216)
+    return torch.linspace(0, 1, n).to(torch.device("cuda", device_index))
+
+
+def pack_fwd(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    m, _ = _maps(flat.device.index)
+    out = torch.empty(FWD_PACKED, device=flat.device) if out is None else out
+    call("nr_pack", ptr(flat), ptr(m), m.numel(), ptr(out), stream_of(flat.device))
+    return out
+
+
+def pack_bwd(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    _, m = _maps(flat.device.index)
+    out = torch.empty(BWD_PACKED, device=flat.device) if out is None else out
+    call("nr_pack", ptr(flat), ptr(m), m.numel(), ptr(out), stream_of(flat.device))
+    return out
+
+
+def mlp_forward(packed: torch.Tensor, *, rays=None, z=None, samples_per_ray=0, x=None,
+                sigma_only=False, save=False):
+    """Fused PE + MLP.  Either (rays (R,8), z (R*spr)) or pre-embedded x (n, 90|63).
+    Returns (out (n,4)|(n,1), saved activations or None)."""
+    if x is not None:
+        x = _dev(x, "x")
+        n, xstride = x.shape[0], x.shape[1]
+    else:
+        rays = _dev(rays, "rays", 8)
+        z = _dev(z, "z")
+        n, xstride = z.numel(), 0
+    dev = packed.device
+    out = torch.empty(n, 1 if sigma_only else 4, device=dev)
+    sv = torch.empty(n * SAVE_PER_SAMPLE, device=dev) if save else None
+    call("nr_mlp_fwd", ptr(packed), ptr(rays), ptr(z), n, int(samples_per_ray), ptr(x), xstride,
+         int(sigma_only), ptr(out), ptr(sv), stream_of(dev))
+    return out, sv
+
+
+def coarse_z(rays, n_samples, use_disp, perturb, u=None, seed=0):
+    rays = _dev(rays, "rays", 8)
+    n_rays = rays.shape[0]
+    z = torch.empty(n_rays, n_samples, device=rays.device)
+    tl = linspace_table(n_samples, rays.device.index)
+    call("nr_coarse_z", ptr(rays), ptr(tl), n_rays, n_samples, int(use_disp), float(perturb),
+         ptr(u), seed, ptr(z), stream_of(rays.device))
+    return z
+
+
+def composite_forward(raw, z, rays, noise, noise_std, seed, rng_stream, white_back,
+                      weights_only=False):
+    """raw (R*S, 4) [rgb, sigma] or (R*S, 1) sigma."""
+    z = _dev(z, "z")
+    n_rays, S = z.shape
+    stride = raw.shape[-1]
+    dev = z.device
+    opac = torch.empty(n_rays, device=dev)
+    w = torch.empty(n_rays, S, device=dev)
+    rgb = None if weights_only else torch.empty(n_rays, 3, device=dev)
+    depth = None if weights_only else torch.empty(n_rays, device=dev)
+    call("nr_composite_fwd", ptr(raw), stride, stride - 1, ptr(z), ptr(rays), ptr(noise),
+         float(noise_std), seed, rng_stream, n_rays, S, int(white_back), int(weights_only),
+         ptr(rgb), ptr(depth), ptr(opac), ptr(w), stream_of(dev))
+    return rgb, depth, opac, w
+
+
+def composite_backward(raw, z, rays, noise, noise_std, seed, rng_stream, white_back,
+                       g_rgb, g_depth, g_opacity):
+    n_rays, S = z.shape
+    g_raw = torch.empty(n_rays * S, 4, device=z.device)
+    call("nr_composite_bwd", ptr(raw), ptr(z), ptr(rays), ptr(noise), float(noise_std), seed,
+         rng_stream, n_rays, S, int(white_back),
+         ptr(None if g_rgb is None else g_rgb.contiguous()),
+         ptr(None if g_depth is None else g_depth.contiguous()),
+         ptr(None if g_opacity is None else g_opacity.contiguous()), ptr(g_raw),
+         stream_of(z.device))
+    return g_raw
+
+
+def sample_pdf(weights, rays, n_importance, u=None, jitter=None, seed=0, z_coarse=None,
+               merge=False):
+    """Importance depths (R, I); with merge=True also the sorted (R, S+I) fine depths."""
+    weights = _dev(weights, "weights")
+    rays = _dev(rays, "rays", 8)
+    n_rays, S = weights.shape
+    dev = weights.device
+    z_pdf = torch.empty(n_rays, n_importance, device=dev)
+    z_fine = torch.empty(n_rays, S + n_importance, device=dev) if merge else None
+    call("nr_sample_pdf", ptr(weights), S, ptr(rays), ptr(z_coarse), ptr(u), ptr(jitter), seed,
+         n_rays, n_importance, ptr(z_pdf), ptr(z_fine), stream_of(dev))
+    return z_pdf, z_fine
+
+
+def embed(x, n_freqs):
+    x = _dev(x, "x", 3)
+    n = x.shape[0]
+    out = torch.empty(n, 3 * (2 * n_freqs + 1), device=x.device)
+    call("nr_embed", ptr(x), n, int(n_freqs), ptr(out), stream_of(x.device))
+    return out
+
+
+def probe_mfma32(a, b):
+    d = torch.empty(32 * 32, device=a.device)
+    call("nr_probe_mfma32", ptr(a), ptr(b), ptr(d), stream_of(a.device))
+    return d.view(32, 32)
+
+
+def layout_query(what: int) -> int:
+    return int(lib().nr_layout_query(what))
+
+
+def np_maps():
+    return packing.build_fwd_map(), packing.build_bwd_map()
+
+
+__all__ = [n for n in dir() if not n.startswith("_") and n not in ("np", "functools")]

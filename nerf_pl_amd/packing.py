@@ -1,0 +1,218 @@
+"""Fragment-order weight packing for the fused MLP kernels.
+
+The fused kernels evaluate every layer in the *transposed* form
+``D[out_feature][sample] = sum_k W[out_feature][k] * X[k][sample]`` on
+``v_mfma_f32_32x32x2_f32`` tiles, so a layer's accumulator (features in
+registers, sample on the lane) is directly the B operand of the next layer.
+MFMA k-step ``g`` of a 256-wide activation therefore pairs the features
+
+    kmap_acc(g, h) = 32*(g>>4) + (g&3) + 8*((g>>2)&3) + 4*h      (h = lane>>5)
+
+and the A operand (weights) must be packed in that k order.  This module builds
+int32 gather maps ``packed[i] = flat_params[map[i]]`` (``-1`` -> 0) once per
+model geometry; ``nr_pack`` (HIP) applies them every step, because the weights
+change every optimizer step.
+
+Packed layout of one layer: ``[g//4][tile][lane][g%4]`` -- one ``float4`` per
+lane per (4 k-steps, 32-row tile), i.e. one fully coalesced 1 KiB wave load.
+
+Positional-encoding k-steps pair features of the same function so that both
+lane halves evaluate the same transcendental (see ``pe_feature``):
+  g=0: (x, y)   g=1: (z, pad)   g=2..: sin pairs   then cos pairs.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+
+W = 256
+WD = 128
+XYZ_CH = 63
+DIR_CH = 27
+PE_KSTEPS = 32
+DIR_KSTEPS = 16
+
+PARAM_ORDER = (
+    [(f"xyz_encoding_{i}.0.weight", f"xyz_encoding_{i}.0.bias") for i in range(1, 9)]
+    + [("xyz_encoding_final.weight", "xyz_encoding_final.bias"),
+       ("dir_encoding.0.weight", "dir_encoding.0.bias"),
+       ("sigma.weight", "sigma.bias"),
+       ("rgb.0.weight", "rgb.0.bias")])
+
+
+def param_shapes():
+    s = OrderedDict()
+    for i in range(1, 9):
+        fan = XYZ_CH if i == 1 else (W + XYZ_CH if i == 5 else W)
+        s[f"xyz_encoding_{i}.0.weight"] = (W, fan)
+        s[f"xyz_encoding_{i}.0.bias"] = (W,)
+    s["xyz_encoding_final.weight"] = (W, W)
+    s["xyz_encoding_final.bias"] = (W,)
+    s["dir_encoding.0.weight"] = (WD, W + DIR_CH)
+    s["dir_encoding.0.bias"] = (WD,)
+    s["sigma.weight"] = (1, W)
+    s["sigma.bias"] = (1,)
+    s["rgb.0.weight"] = (3, WD)
+    s["rgb.0.bias"] = (3,)
+    return s
+
+
+def param_offsets():
+    """Offsets of each parameter inside the flat fp32 parameter buffer."""
+    offs, o = OrderedDict(), 0
+    for name, shp in param_shapes().items():
+        offs[name] = (o, shp)
+        o += int(np.prod(shp))
+    return offs, o
+
+
+N_PARAMS = param_offsets()[1]   # 595,844
+
+
+# -- k-step feature maps ------------------------------------------------------
+def kmap_acc(g, h):
+    g = np.asarray(g)
+    return 32 * (g >> 4) + (g & 3) + 8 * ((g >> 2) & 3) + 4 * np.asarray(h)
+
+
+def _pe_feature(g, h, n_pairs):
+    """Original Embedding channel (or -1 for padding) of PE k-step g, half h.
+    n_pairs: 15 for xyz (30 sin / 30 cos), 6 for dir (12 / 12)."""
+    if g == 0:
+        return h                      # x | y
+    if g == 1:
+        return 2 if h == 0 else -1    # z | pad
+    if g < 2 + n_pairs:
+        m = (g - 2) + n_pairs * h
+        return 3 + 6 * (m // 3) + (m % 3)   # sin(2^(m//3) * x_(m%3))
+    if g < 2 + 2 * n_pairs:
+        m = (g - 2 - n_pairs) + n_pairs * h
+        return 6 + 6 * (m // 3) + (m % 3)   # cos(...)
+    return -1
+
+
+def pe_feature(g, h):
+    return _pe_feature(g, h, 15)
+
+
+def dir_feature(g, h):
+    return _pe_feature(g, h, 6)
+
+
+PE_MAP = np.array([[pe_feature(g, h) for h in (0, 1)] for g in range(PE_KSTEPS)])
+DIR_MAP = np.array([[dir_feature(g, h) for h in (0, 1)] for g in range(DIR_KSTEPS)])
+
+
+def _frag_coords(ksteps, ntiles):
+    """(g, T, lane) for every element of a packed layer, in packed order."""
+    e = np.arange(ksteps * ntiles * 64)
+    grp, rem = e // (ntiles * 256), e % (ntiles * 256)
+    T = rem // 256
+    lane = (rem % 256) // 4
+    kk = rem % 4
+    return grp * 4 + kk, T, lane
+
+
+def _fwd_layer_map(w_name, segs, ntiles, offs):
+    """segs: list of (ksteps, kind, col_offset); kind in {'acc','pe','dir'}."""
+    w_off, (rows, fan) = offs[w_name]
+    parts = []
+    for ksteps, kind, col0 in segs:
+        g, T, lane = _frag_coords(ksteps, ntiles)
+        h = lane >> 5
+        row = 32 * T + (lane & 31)
+        if kind == "acc":
+            col = kmap_acc(g, h)
+        elif kind == "pe":
+            col = PE_MAP[g, h]
+        else:
+            col = DIR_MAP[g, h]
+        ok = (col >= 0) & (row < rows)
+        idx = np.where(ok, w_off + row * fan + col0 + np.maximum(col, 0), -1)
+        parts.append(idx)
+    # interleave segments in k order: each segment is a whole number of 4-k groups
+    return np.concatenate(parts)
+
+
+def _bwd_layer_map(w_name, k_out, ntiles, col0, offs):
+    """Transposed layer: k runs over the layer's OUTPUT features (acc layout),
+    tiles over its input features starting at column col0."""
+    w_off, (rows, fan) = offs[w_name]
+    g, T, lane = _frag_coords(k_out // 2, ntiles)
+    h = lane >> 5
+    r = kmap_acc(g, h)          # W row (output feature of the layer)
+    c = col0 + 32 * T + (lane & 31)
+    return w_off + r * fan + c
+
+
+def _head_map(offs):
+    m = []
+    for i in range(1, 9):
+        o, _ = offs[f"xyz_encoding_{i}.0.bias"]
+        m.append(o + np.arange(W))
+    m.append(offs["xyz_encoding_final.bias"][0] + np.arange(W))
+    m.append(offs["dir_encoding.0.bias"][0] + np.arange(WD))
+    m.append(offs["sigma.weight"][0] + np.arange(W))
+    m.append(np.array([offs["sigma.bias"][0], -1, -1, -1]))
+    m.append(offs["rgb.0.weight"][0] + np.arange(3 * WD))
+    m.append(np.array([offs["rgb.0.bias"][0] + i for i in range(3)] + [-1]))
+    return np.concatenate(m)
+
+
+# offsets (floats) inside the packed buffers -- mirrored in csrc/layout.h
+FWD_LAYERS = OrderedDict([
+    ("L1", (PE_KSTEPS, 8)),
+    ("L2", (128, 8)), ("L3", (128, 8)), ("L4", (128, 8)),
+    ("L5", (PE_KSTEPS + 128, 8)),
+    ("L6", (128, 8)), ("L7", (128, 8)), ("L8", (128, 8)),
+    ("final", (128, 8)),
+    ("dir", (128 + DIR_KSTEPS, 4)),
+])
+BWD_LAYERS = OrderedDict([
+    ("dirT", (64, 8)), ("finalT", (128, 8)),
+    ("L8T", (128, 8)), ("L7T", (128, 8)), ("L6T", (128, 8)), ("L5T", (128, 8)),
+    ("L4T", (128, 8)), ("L3T", (128, 8)), ("L2T", (128, 8)),
+])
+HEAD_SIZE = 8 * W + W + WD + W + 4 + 3 * WD + 4   # 3080
+
+
+def layer_offsets(layers):
+    offs, o = OrderedDict(), 0
+    for k, (ks, nt) in layers.items():
+        offs[k] = o
+        o += ks * nt * 64
+    return offs, o
+
+
+def build_fwd_map():
+    offs, _ = param_offsets()
+    L = lambda i: f"xyz_encoding_{i}.0.weight"  # noqa: E731
+    parts = [_fwd_layer_map(L(1), [(PE_KSTEPS, "pe", 0)], 8, offs)]
+    for i in (2, 3, 4):
+        parts.append(_fwd_layer_map(L(i), [(128, "acc", 0)], 8, offs))
+    parts.append(_fwd_layer_map(L(5), [(PE_KSTEPS, "pe", 0), (128, "acc", XYZ_CH)], 8, offs))
+    for i in (6, 7, 8):
+        parts.append(_fwd_layer_map(L(i), [(128, "acc", 0)], 8, offs))
+    parts.append(_fwd_layer_map("xyz_encoding_final.weight", [(128, "acc", 0)], 8, offs))
+    parts.append(_fwd_layer_map("dir_encoding.0.weight",
+                                [(128, "acc", 0), (DIR_KSTEPS, "dir", W)], 4, offs))
+    parts.append(_head_map(offs))
+    m = np.concatenate(parts).astype(np.int32)
+    assert m.size == layer_offsets(FWD_LAYERS)[1] + HEAD_SIZE
+    return m
+
+
+def build_bwd_map():
+    offs, _ = param_offsets()
+    L = lambda i: f"xyz_encoding_{i}.0.weight"  # noqa: E731
+    parts = [_bwd_layer_map("dir_encoding.0.weight", WD, 8, 0, offs),
+             _bwd_layer_map("xyz_encoding_final.weight", W, 8, 0, offs)]
+    for i in (8, 7, 6):
+        parts.append(_bwd_layer_map(L(i), W, 8, 0, offs))
+    parts.append(_bwd_layer_map(L(5), W, 8, XYZ_CH, offs))
+    for i in (4, 3, 2):
+        parts.append(_bwd_layer_map(L(i), W, 8, 0, offs))
+    m = np.concatenate(parts).astype(np.int32)
+    assert m.size == layer_offsets(BWD_LAYERS)[1]
+    return m
