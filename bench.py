@@ -1,0 +1,283 @@
+"""Training-step throughput of the drop-in render_rays path on MI355X.
+
+One step = one NeRFSystem.training_step of the reference (train.py:103-117)
+on synthetic Blender-lego 400x400 rays: gather B=4096 rays per rank from an
+HBM-resident ray pool -> render_rays (64 coarse + 128 fine, perturb=1,
+noise_std=1: opt.py defaults) -> MSE(coarse)+MSE(fine) -> backward ->
+[RCCL all-reduce of the 4.77 MB gradient when N>1] -> Adam(lr=5e-4).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0).  ``value`` = rays/s over all ranks.  The
+``roofline`` object is for the dominant kernel, timed with HIP events around
+each of its launches inside the timed region; ``cpu_baseline`` times the CPU
+oracle (the reference algorithm restated in PyTorch-CPU, pinned to the
+reference by tests/golden) on a bounded sample on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
+HBM_PEAK_GBS = 8000.0
+# algorithmic FLOP per sample: forward, data-grad, weight-grad
+FLOP_FWD = 1_186_816
+FLOP_DGRAD = 1_115_392
+FLOP_WGRAD = 1_186_816
+FLOP_TRAIN = FLOP_FWD + FLOP_DGRAD + FLOP_WGRAD   # 3,489,024
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4096, help="rays per rank per step")
+    ap.add_argument("--img", type=int, default=400)
+    ap.add_argument("--poses", type=int, default=100)
+    ap.add_argument("--n-samples", type=int, default=64)
+    ap.add_argument("--n-importance", type=int, default=128)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
+                    help="budget of the CPU oracle sample (0 disables)")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    return ap.parse_args()
+
+
+class KernelTimer:
+    """HIP events around every launch of the instrumented kernels (on the
+    stream they are launched on: torch's current stream)."""
+
+    def __init__(self):
+        self.events = {}
+        self.enabled = False
+
+    def wrap(self, mod, fname, tag_fn):
+        orig = getattr(mod, fname)
+
+        def wrapped(*a, **k):
+            if not self.enabled:
+                return orig(*a, **k)
+            tag, n = tag_fn(*a, **k)
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = orig(*a, **k)
+            e.record()
+            self.events.setdefault(tag, []).append((s, e, n))
+            return r
+        setattr(mod, fname, wrapped)
+
+    def summary(self):
+        out = {}
+        for tag, lst in self.events.items():
+            ms = [s.elapsed_time(e) for s, e, _ in lst]
+            out[tag] = dict(launches=len(lst), total_ms=sum(ms), avg_ms=sum(ms) / len(ms),
+                            samples=sum(n for *_, n in lst) / len(lst))
+        return out
+
+
+def install_timers(timer):
+    from nerf_pl_amd import _lib, ops
+
+    def call_tag(name, *a):
+        if name == "nr_mlp_fwd":
+            return ("mlp_fwd_sigma" if a[7] else "mlp_fwd"), int(a[3])
+        if name == "nr_mlp_bwd":
+            return "mlp_bwd_dgrad", int(a[5])
+        if name == "nr_wgrad":
+            return "mlp_wgrad", int(a[2])
+        return name[3:], 0
+
+    orig_call = _lib.call
+
+    def timed_call(name, *a):
+        if not timer.enabled:
+            return orig_call(name, *a)
+        tag, n = call_tag(name, *a)
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        orig_call(name, *a)
+        e.record()
+        timer.events.setdefault(tag, []).append((s, e, n))
+
+    _lib.call = timed_call
+    ops.call = timed_call
+    import nerf_pl_amd.functions as F
+    F.call = timed_call
+
+
+def cpu_baseline(args, budget_s):
+    """Oracle (reference algorithm, PyTorch CPU) training step on a bounded
+    sample of the same workload: B_cpu rays, same sample counts."""
+    from oracle import nerf_oracle as O
+    from nerf_pl_amd.rays import blender_rays
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    rays_all = blender_rays(args.img, 1)
+    b = 256
+    params = [{k: v.requires_grad_(True) for k, v in O.make_params(s).items()} for s in (1, 2)]
+    opt = torch.optim.Adam([p for d in params for p in d.values()], lr=5e-4)
+    n_rays, t0, steps = 0, time.perf_counter(), 0
+    while True:
+        idx = torch.randint(0, rays_all.shape[0], (b,))
+        rays = rays_all[idx]
+        tgt = torch.rand(b, 3)
+        res = O.render_rays(params, rays, args.n_samples, False, 1.0, 1.0, args.n_importance,
+                            32768, False)
+        loss = O.mse_loss(res, tgt)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        n_rays += b
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and steps >= 2:
+            break
+    return dict(value=n_rays / el, unit="rays/s", cores=threads, kind="port",
+                sample=f"{steps} oracle training steps x {b} rays (64+128 samples, fwd+bwd+Adam) "
+                       f"in {el:.1f} s, torch CPU {threads} threads")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from nerf_pl_amd import Embedding, NeRF, render_rays
+    from nerf_pl_amd.rays import blender_rays
+
+    timer = KernelTimer()
+    if not args.no_kernel_timing:
+        install_timers(timer)
+
+    # HBM-resident ray pool (datasets/blender.py: all rays of all train images)
+    torch.manual_seed(1234 + rank)
+    pool = blender_rays(args.img, args.poses, near=1.0, far=200.0, device=dev).contiguous()
+    pool_rgb = torch.rand(pool.shape[0], 3, device=dev)
+    torch.manual_seed(0)                      # identical initial weights on every rank
+    models = [NeRF().to(dev), NeRF().to(dev)]
+    emb = [Embedding(3, 10), Embedding(3, 4)]
+    params = [p for m in models for p in m.parameters()]
+    opt = torch.optim.Adam(params, lr=5e-4, eps=1e-8)
+    gen = torch.Generator(device=dev).manual_seed(99 + rank)
+
+    def step():
+        idx = torch.randint(0, pool.shape[0], (args.batch,), device=dev, generator=gen)
+        rays = pool.index_select(0, idx)
+        rgbs = pool_rgb.index_select(0, idx)
+        res = render_rays(models, emb, rays, args.n_samples, False, 1.0, 1.0,
+                          args.n_importance, 32768, False)
+        loss = torch.mean((res["rgb_coarse"] - rgbs) ** 2) + torch.mean((res["rgb_fine"] - rgbs) ** 2)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if world > 1:
+            flat = torch.cat([p.grad.reshape(-1) for p in params])
+            dist.all_reduce(flat)
+            flat.div_(world)
+            off = 0
+            for p in params:
+                n = p.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p))
+                off += n
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    timer.enabled = False
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    ms = el / args.steps * 1e3
+    rays_per_s = args.batch * world * args.steps / el
+
+    ks = timer.summary()
+    roof = None
+    if ks:
+        flop = {"mlp_fwd": FLOP_FWD, "mlp_bwd_dgrad": FLOP_DGRAD, "mlp_wgrad": FLOP_WGRAD}
+        dom = max((k for k in ks if k in flop), key=lambda k: ks[k]["total_ms"])
+        d = ks[dom]
+        # the dominant kernel's largest launches (fine pass) set the roofline
+        big = [(s.elapsed_time(e), n) for s, e, n in timer.events[dom]]
+        nmax = max(n for _, n in big)
+        durs = [t for t, n in big if n == nmax]
+        avg = sum(durs) / len(durs)
+        ach = flop[dom] * nmax / (avg * 1e-3) / 1e12
+        roof = dict(bound="mfma", kernel=dom, achieved=round(ach, 2), peak=FP32_MFMA_PEAK_TF,
+                    unit="TFLOP/s", frac=round(ach / FP32_MFMA_PEAK_TF, 4), traffic=None,
+                    samples_per_launch=nmax, avg_launch_ms=round(avg, 4),
+                    flop_per_sample=flop[dom])
+        d["share_of_step"] = d["total_ms"] / (ms * args.steps)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
+        cpu = cpu_baseline(args, args.cpu_baseline_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "rays/sec (64c+128f) Blender-lego 400^2 training step",
+            "value": round(rays_per_s, 1),
+            "unit": "rays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (Blender-lego 400x400 camera orbit rays, random targets, "
+                    "seeded default-init NeRF coarse+fine)",
+            "config": {"workload": "cfg2: Blender lego 400x400, 64 coarse + 128 fine, "
+                                   f"batch {args.batch} rays/rank, perturb=1, noise_std=1, "
+                                   "MSE coarse+fine, Adam lr 5e-4",
+                       "global_batch": args.batch * world,
+                       "samples_per_ray": args.n_samples + args.n_importance,
+                       "parallelism": f"dp{world}"},
+            "model_tflops": round(rays_per_s * (args.n_samples * FLOP_TRAIN
+                                                + (args.n_samples + args.n_importance)
+                                                * FLOP_TRAIN) / 1e12, 2),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv
+                            for kk, vv in v.items()} for k, v in ks.items()},
+            "final_loss": round(loss.item(), 5),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,119 @@
+"""Autograd functions binding the HIP forward/backward kernels.
+
+``_FusedMLP``: fused PE + MLP forward (saving activations when any parameter
+needs a gradient); backward = fused data-gradient chain (``nr_mlp_bwd``) then
+the grouped split-K weight-gradient GEMM (``nr_wgrad``), returning one gradient
+per ``NeRF`` parameter (views into one flat buffer, named_parameters order).
+
+``_Composite``: volume compositing forward/backward (``nr_composite_*``).
+"""
+from __future__ import annotations
+
+import functools
+
+import torch
+
+from . import ops, packing
+from ._lib import call, stream_of
+
+
+@functools.lru_cache(maxsize=None)
+def _wgrad_workspace(device_index: int) -> torch.Tensor:
+    from ._lib import lib
+    nbytes = int(lib().nr_wgrad_workspace_bytes(0))
+    return torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", device_index))
+
+
+_SHAPES = list(packing.param_shapes().items())
+# parameters the sigma-only graph does not reach (reference autograd leaves them None)
+_SIGMA_ONLY_UNUSED = {"xyz_encoding_final.weight", "xyz_encoding_final.bias",
+                      "dir_encoding.0.weight", "dir_encoding.0.bias",
+                      "rgb.0.weight", "rgb.0.bias"}
+
+
+class _FusedMLP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, rays, z, spr, x, sigma_only, *params):
+        train = any(ctx.needs_input_grad[6:])
+        if train and sigma_only and x is not None:
+            raise NotImplementedError("nerf_pl_amd: training NeRF.forward(x, sigma_only=True) on "
+                                      "pre-embedded input is not supported; use render_rays")
+        packed_f, packed_b = model.packed(backward=train)
+        # a sigma-only graph is trained through the full kernel (rgb gradient 0)
+        kern_sigma_only = sigma_only and not train
+        out, save = ops.mlp_forward(packed_f, rays=rays, z=z, samples_per_ray=spr, x=x,
+                                    sigma_only=kern_sigma_only, save=train)
+        if train:
+            ctx.save_for_backward(out, save, packed_f, packed_b)
+            ctx.sigma_only = sigma_only
+        if sigma_only and not kern_sigma_only:
+            out = out[:, 3:4].contiguous()
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        out, save, packed_f, packed_b = ctx.saved_tensors
+        n = out.shape[0]
+        dev = out.device
+        if ctx.sigma_only:
+            g4 = torch.zeros(n, 4, device=dev)
+            g4[:, 3:4] = g_out
+            g_out = g4
+        grad_ws = torch.empty(n * ops.GRAD_PER_SAMPLE, device=dev)
+        g_out = g_out.contiguous()
+        call("nr_mlp_bwd", packed_b.data_ptr(), packed_f.data_ptr(), out.data_ptr(),
+             g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), stream_of(dev))
+        gflat = torch.empty(packing.N_PARAMS, device=dev)
+        ws = _wgrad_workspace(dev.index)
+        call("nr_wgrad", save.data_ptr(), grad_ws.data_ptr(), n, ws.data_ptr(),
+             gflat.data_ptr(), stream_of(dev))
+        grads, off = [], 0
+        for name, shp in _SHAPES:
+            k = 1
+            for d in shp:
+                k *= d
+            g = gflat[off:off + k].view(shp)
+            off += k
+            grads.append(None if (ctx.sigma_only and name in _SIGMA_ONLY_UNUSED) else g)
+        return (None,) * 6 + tuple(grads)
+
+
+def mlp_apply(model, *, rays=None, z=None, spr=0, x=None, sigma_only=False):
+    """Run ``model`` (a nerf_pl_amd.NeRF) on rays+depths or on embedded x."""
+    if x is not None and x.requires_grad:
+        raise NotImplementedError("nerf_pl_amd: gradients w.r.t. the embedded input are not "
+                                  "produced (the reference never needs them)")
+    params = model.ordered_params()
+    if z is not None:
+        z = z.reshape(-1)
+    if not any(p.requires_grad for p in params) or not torch.is_grad_enabled():
+        packed_f, _ = model.packed()
+        out, _ = ops.mlp_forward(packed_f, rays=rays, z=z, samples_per_ray=spr, x=x,
+                                 sigma_only=sigma_only)
+        return out
+    return _FusedMLP.apply(model, rays, z, spr, x, sigma_only, *params)
+
+
+class _Composite(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, raw, z, rays, noise, noise_std, seed, stream, white_back):
+        rgb, depth, opac, w = ops.composite_forward(raw, z, rays, noise, noise_std, seed, stream,
+                                                    white_back)
+        ctx.save_for_backward(raw, z, rays, noise if noise is not None else torch.empty(0))
+        ctx.cfg = (noise is not None, noise_std, seed, stream, white_back)
+        ctx.mark_non_differentiable(w)
+        return rgb, depth, opac, w
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_opac, g_w):   # noqa: ARG004 -- weights not differentiable
+        raw, z, rays, noise = ctx.saved_tensors
+        has_noise, noise_std, seed, stream, white_back = ctx.cfg
+        g_raw = ops.composite_backward(raw, z, rays, noise if has_noise else None, noise_std, seed,
+                                       stream, white_back, g_rgb, g_depth, g_opac)
+        return g_raw, None, None, None, None, None, None, None
+
+
+def composite_apply(raw, z, rays, noise, noise_std, seed, stream, white_back):
+    if torch.is_grad_enabled() and raw.requires_grad:
+        return _Composite.apply(raw, z, rays, noise, noise_std, seed, stream, white_back)
+    return ops.composite_forward(raw, z, rays, noise, noise_std, seed, stream, white_back)
