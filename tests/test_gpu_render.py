@@ -164,7 +164,8 @@ def test_training_steps_reduce_loss():
     from nerf_pl_amd.rays import blender_rays
     torch.manual_seed(0)
     rays = blender_rays(32, 1, near=2.0, far=6.0, device=DEV)[:512].contiguous()
-    target = torch.rand(512, 3, device=DEV)
+    # a learnable target: a smooth colour field over ray directions
+    target = (0.5 + 0.4 * torch.sin(3 * rays[:, 3:6])).contiguous()
     models = [NeRF().to(DEV), NeRF().to(DEV)]
     opt = torch.optim.Adam([p for m in models for p in m.parameters()], lr=5e-4)
     losses = []
