@@ -41,31 +41,93 @@
 #define NR_B_L2T (NR_B_L3T + NR_PL(128, 8))
 #define NR_B_TOTAL (NR_B_L2T + NR_PL(128, 8))
 
-// ---- saved activations (forward, training mode) ---------------------------
-// One buffer of NR_SAVE_PER_SAMPLE * n floats, segments row-major [n][width]:
-//   pe[n][64] (paired k order: col 2g+h), h1..h8[n][256], feat[n][256],
-//   hdir[n][128], dirpe[n][32] (paired k order)
-#define NR_SAVE_PER_SAMPLE (64 + 8 * 256 + 256 + 128 + 32)
+// ---- saved activations / gradients: BLOCK-NATIVE layout ------------------
+// Samples are grouped in blocks of 32 (one wave).  A width-W activation of a
+// block is stored exactly as the wave's accumulators hold it: feature
+// f = 32t + 8q + 4h + e of sample j (lane l = 32h + j) lives at
+//     [block][t][q][lane][e]        (W*32 floats per block)
+// so every wave store/load instruction moves one contiguous 1 KiB.
+// PE segments hold the packed k-step values pe[g] as [block][g/4][lane][g%4].
+// ReLU masks are bits: word d of a lane covers tiles 2d, 2d+1 (bit 16*(t&1)+r).
+#define NR_BLK 32
+#define NR_NATIVE(w) ((w) * NR_BLK)
+#define NR_MASK_LAYERS 9          // h1..h8, hdir
+#define NR_SAVE_PER_BLOCK (NR_NATIVE(64) + 8 * NR_NATIVE(256) + NR_NATIVE(256) + \
+                           NR_NATIVE(128) + NR_NATIVE(32) + NR_MASK_LAYERS * 256)
 struct NrSave {
-    float* pe; float* h[8]; float* feat; float* hdir; float* dirpe;
-    __host__ __device__ NrSave(float* base, int64_t n) {
+    float* pe; float* h[8]; float* feat; float* hdir; float* dirpe; uint32_t* mask;
+    __host__ __device__ NrSave(float* base, int64_t nb) {
         pe = base;
-        for (int l = 0; l < 8; ++l) h[l] = base + 64 * n + (int64_t)l * 256 * n;
-        feat = base + 64 * n + 8 * 256 * n;
-        hdir = feat + 256 * n;
-        dirpe = hdir + 128 * n;
+        for (int l = 0; l < 8; ++l) h[l] = base + NR_NATIVE(64) * nb + (int64_t)l * NR_NATIVE(256) * nb;
+        feat = base + (NR_NATIVE(64) + 8 * NR_NATIVE(256)) * nb;
+        hdir = feat + NR_NATIVE(256) * nb;
+        dirpe = hdir + NR_NATIVE(128) * nb;
+        mask = reinterpret_cast<uint32_t*>(dirpe + NR_NATIVE(32) * nb);
     }
 };
 
-// ---- per-layer pre-activation gradients (backward) ------------------------
-//   dz1..dz8[n][256], dfeat[n][256], dzdir[n][128], dhead[n][4]=(drgb_z, dsigma)
-#define NR_GRAD_PER_SAMPLE (8 * 256 + 256 + 128 + 4)
+//   dz1..dz8, dfeat (256 wide), dzdir (128), dhead [block][j][4] = (dz_rgb, dsigma)
+#define NR_GRAD_PER_BLOCK (9 * NR_NATIVE(256) + NR_NATIVE(128) + NR_BLK * 4)
 struct NrGrad {
     float* dz[8]; float* dfeat; float* dzdir; float* dhead;
-    __host__ __device__ NrGrad(float* base, int64_t n) {
-        for (int l = 0; l < 8; ++l) dz[l] = base + (int64_t)l * 256 * n;
-        dfeat = base + 8 * 256 * n;
-        dzdir = dfeat + 256 * n;
-        dhead = dzdir + 128 * n;
+    __host__ __device__ NrGrad(float* base, int64_t nb) {
+        for (int l = 0; l < 8; ++l) dz[l] = base + (int64_t)l * NR_NATIVE(256) * nb;
+        dfeat = base + 8 * NR_NATIVE(256) * nb;
+        dzdir = dfeat + NR_NATIVE(256) * nb;
+        dhead = dzdir + NR_NATIVE(128) * nb;
     }
 };
+
+// keep x where mask bit b of word w is set, else +0 (ReLU backward)
+__device__ __forceinline__ float nr_mask_bit(float x, uint32_t w, int b) {
+    const uint32_t keep = 0u - ((w >> b) & 1u);
+    return __uint_as_float(__float_as_uint(x) & keep);
+}
+
+// On-demand segment addresses (keeps scalar register pressure low in the
+// fully unrolled kernels): offsets in floats from the buffer base, nb blocks.
+__host__ __device__ __forceinline__ int64_t nr_sv_pe(int64_t) { return 0; }
+__host__ __device__ __forceinline__ int64_t nr_sv_h(int l, int64_t nb) {
+    return (NR_NATIVE(64) + (int64_t)l * NR_NATIVE(256)) * nb;
+}
+__host__ __device__ __forceinline__ int64_t nr_sv_feat(int64_t nb) { return nr_sv_h(8, nb); }
+__host__ __device__ __forceinline__ int64_t nr_sv_hdir(int64_t nb) { return nr_sv_h(9, nb); }
+__host__ __device__ __forceinline__ int64_t nr_sv_dirpe(int64_t nb) {
+    return nr_sv_hdir(nb) + NR_NATIVE(128) * nb;
+}
+__host__ __device__ __forceinline__ int64_t nr_sv_mask(int64_t nb) {
+    return nr_sv_dirpe(nb) + NR_NATIVE(32) * nb;
+}
+__host__ __device__ __forceinline__ int64_t nr_gd_dz(int l, int64_t nb) {   // l = 0..8 (8 = dfeat)
+    return (int64_t)l * NR_NATIVE(256) * nb;
+}
+__host__ __device__ __forceinline__ int64_t nr_gd_dzdir(int64_t nb) { return nr_gd_dz(9, nb); }
+__host__ __device__ __forceinline__ int64_t nr_gd_dhead(int64_t nb) {
+    return nr_gd_dzdir(nb) + NR_NATIVE(128) * nb;
+}
+
+// wave-level helpers shared by the fused kernels ---------------------------
+template <int NT>
+__device__ __forceinline__ void store_native(const f32x16 (&acc)[NT], float* __restrict__ blk,
+                                             int lane) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            f32x4 v = {acc[t][4 * q + 0], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+            *reinterpret_cast<f32x4*>(blk + ((t * 4 + q) * 64 + lane) * 4) = v;
+        }
+}
+
+template <int NT>
+__device__ __forceinline__ void store_mask(const f32x16 (&acc)[NT], uint32_t* __restrict__ m,
+                                           int lane) {
+    // acc is post-ReLU (exactly +0 or positive): bit = (bits(x) != 0), VALU only
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            w[t >> 1] |= min(__float_as_uint(acc[t][r]), 1u) << (16 * (t & 1) + r);
+    *reinterpret_cast<uint4*>(m + lane * 4) = make_uint4(w[0], w[1], w[2], w[3]);
+}

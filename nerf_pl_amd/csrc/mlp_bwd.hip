@@ -3,9 +3,9 @@
 // Same geometry as the forward: one wave carries 32 samples backwards through
 // every layer in transposed form D[in_feature][sample] = W^T[in][out] dz[out][sample]
 // on v_mfma_f32_32x32x2_f32, with the transposed weights pre-packed in fragment
-// order (packing.py BWD_LAYERS).  ReLU masks come from the saved activations.
-// Every layer's pre-activation gradient dz is written out row-major [n][width]
-// for the weight-gradient GEMMs (wgrad.hip).
+// order (packing.py BWD_LAYERS).  ReLU masks are the forward's bit masks.
+// Every layer's pre-activation gradient dz is written out in the block-native
+// layout (layout.h) for the weight-gradient GEMMs (wgrad.hip).
 #include "layout.h"
 
 namespace {
@@ -51,28 +51,14 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[NT]) {
     for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
 }
 
-// acc *= [h > 0] with h the saved post-ReLU activation row (threshold_backward)
+// ReLU backward with the forward's mask bits (one uint4 per lane per layer)
 template <int NT>
-__device__ __forceinline__ void relu_mask(f32x16 (&acc)[NT], const float* __restrict__ row, int h) {
+__device__ __forceinline__ void relu_mask(f32x16 (&acc)[NT], uint4 m) {
+    const uint32_t w[4] = {m.x, m.y, m.z, m.w};
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(row + 32 * t + 8 * q + 4 * h);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[t][4 * q + e] = v[e] > 0.f ? acc[t][4 * q + e] : 0.f;
-        }
-}
-
-template <int NT>
-__device__ __forceinline__ void store_rows(const f32x16 (&acc)[NT], float* __restrict__ row, int h) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            f32x4 v = {acc[t][4 * q + 0], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
-            *reinterpret_cast<f32x4*>(row + 32 * t + 8 * q + 4 * h) = v;
-        }
+        for (int r = 0; r < 16; ++r) acc[t][r] = nr_mask_bit(acc[t][r], w[t >> 1], 16 * (t & 1) + r);
 }
 
 struct BwdArgs {
@@ -89,53 +75,58 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
-    const int s_raw = (blockIdx.x * kWaves + wave) * 32 + (lane & 31);
+    const int blk = blockIdx.x * kWaves + wave;
+    const int nb = (a.n + 31) / 32;
+    if (blk >= nb) return;                      // no barriers in this kernel
+    const int s_raw = blk * 32 + (lane & 31);
     const bool valid = s_raw < a.n;
     const int s = valid ? s_raw : a.n - 1;
     const float* PB = a.packed_bwd;
     const float* H = a.packed_fwd + NR_F_HEAD;
-    NrSave sv(const_cast<float*>(a.save), a.n);
-    NrGrad gd(a.grad, a.n);
+    const float* SV = a.save;
+    float* const GD = a.grad;
+    const uint4* mask = reinterpret_cast<const uint4*>(SV + nr_sv_mask(nb)) +
+                        (size_t)blk * NR_MASK_LAYERS * 64 + lane;   // [layer][lane]
 
     const f32x4 go = *reinterpret_cast<const f32x4*>(a.g_out + (size_t)s * 4);
     const f32x4 yo = *reinterpret_cast<const f32x4*>(a.out + (size_t)s * 4);
-    // sigmoid backward: grad * (1 - y) * y  (ATen sigmoid_backward)
+    // sigmoid backward: grad * (1 - y) * y  (ATen sigmoid_backward); tail lanes -> 0
     float dzr[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) dzr[c] = go[c] * (1.f - yo[c]) * yo[c];
-    const float dsig = go[3];
-    if (valid && h == 0) {
+    for (int c = 0; c < 3; ++c) dzr[c] = valid ? go[c] * (1.f - yo[c]) * yo[c] : 0.f;
+    const float dsig = valid ? go[3] : 0.f;
+    if (h == 0) {
         f32x4 v = {dzr[0], dzr[1], dzr[2], dsig};
-        *reinterpret_cast<f32x4*>(gd.dhead + (size_t)s * 4) = v;
+        *reinterpret_cast<f32x4*>(GD + nr_gd_dhead(nb) + ((size_t)blk * 32 + (lane & 31)) * 4) = v;
     }
 
     // d hdir = W_rgb^T dz_rgb, masked by the dir-layer ReLU -> dz_dir (128)
     f32x16 C[4];
     {
-        const float* hrow = sv.hdir + (size_t)s * 128;
+        const uint4 mk = mask[8 * 64];
+        const uint32_t mw[2] = {mk.x, mk.y};
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int f = 32 * t + 8 * q + 4 * h;
-                const f32x4 hv = *reinterpret_cast<const f32x4*>(hrow + f);
                 const f32x4 w0 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + f);
                 const f32x4 w1 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 128 + f);
                 const f32x4 w2 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 256 + f);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float d = fmaf(w2[e], dzr[2], fmaf(w1[e], dzr[1], w0[e] * dzr[0]));
-                    C[t][4 * q + e] = hv[e] > 0.f ? d : 0.f;
+                    C[t][4 * q + e] = nr_mask_bit(d, mw[t >> 1], 16 * (t & 1) + 4 * q + e);
                 }
             }
-        if (valid) store_rows<4>(C, gd.dzdir + (size_t)s * 128, h);
+        store_native<4>(C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_NATIVE(128), lane);
     }
 
     f32x16 A[8], B[8];
     // d feat = W_dir[:, :256]^T dz_dir   (xyz_encoding_final has no activation)
     zero<8>(A);
     mm_acc<64, 8>(PB + NR_B_DIRT, lane, A, [&](int g) { return C[g >> 4][g & 15]; });
-    if (valid) store_rows<8>(A, gd.dfeat + (size_t)s * 256, h);
+    store_native<8>(A, GD + nr_gd_dz(8, nb) + (size_t)blk * NR_NATIVE(256), lane);
 
     // d h8 = W_final^T dfeat + W_sigma^T dsigma, masked by h8
 #pragma unroll
@@ -146,15 +137,21 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) B[t][4 * q + e] = w[e] * dsig;
         }
-    mm_acc<128, 8>(PB + NR_B_FINALT, lane, B, [&](int g) { return A[g >> 4][g & 15]; });
-    relu_mask<8>(B, sv.h[7] + (size_t)s * 256, h);
-    if (valid) store_rows<8>(B, gd.dz[7] + (size_t)s * 256, h);
+    {
+        const uint4 mk = mask[7 * 64];
+        mm_acc<128, 8>(PB + NR_B_FINALT, lane, B, [&](int g) { return A[g >> 4][g & 15]; });
+        relu_mask<8>(B, mk);
+        store_native<8>(B, GD + nr_gd_dz(7, nb) + (size_t)blk * NR_NATIVE(256), lane);
+    }
 
-#define NR_BACK(DST, SRC, LOFF, L)                                                    \
-    zero<8>(DST);                                                                      \
-    mm_acc<128, 8>(PB + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; });  \
-    relu_mask<8>(DST, sv.h[L - 1] + (size_t)s * 256, h);                               \
-    if (valid) store_rows<8>(DST, gd.dz[L - 1] + (size_t)s * 256, h);
+#define NR_BACK(DST, SRC, LOFF, L)                                                          \
+    {                                                                                        \
+        const uint4 mk = mask[(L - 1) * 64];                                                 \
+        zero<8>(DST);                                                                        \
+        mm_acc<128, 8>(PB + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; });    \
+        relu_mask<8>(DST, mk);                                                               \
+        store_native<8>(DST, GD + nr_gd_dz(L - 1, nb) + (size_t)blk * NR_NATIVE(256), lane); \
+    }
 
     NR_BACK(A, B, NR_B_L8T, 7)   // dz7 = (W8^T dz8) * [h7 > 0]
     NR_BACK(B, A, NR_B_L7T, 6)

@@ -72,19 +72,6 @@ __device__ __forceinline__ void relu(f32x16 (&acc)[NT]) {
         for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] > 0.f ? acc[t][r] : 0.f;
 }
 
-// store the accumulator rows of one sample: row = dst + sample*width, feature
-// 32t + 8q + 4h + e lives in register 4q+e of tile t.
-template <int NT>
-__device__ __forceinline__ void store_rows(const f32x16 (&acc)[NT], float* __restrict__ row, int h) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            f32x4 v = {acc[t][4 * q + 0], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
-            *reinterpret_cast<f32x4*>(row + 32 * t + 8 * q + 4 * h) = v;
-        }
-}
-
 // <w, acc> over this lane's features, then summed over both lane halves.
 template <int NT>
 __device__ __forceinline__ float head_dot(const f32x16 (&acc)[NT], const float* __restrict__ w, int h) {
@@ -157,13 +144,15 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
-    const int s_raw = (blockIdx.x * kWaves + wave) * 32 + (lane & 31);
+    const int blk = blockIdx.x * kWaves + wave;           // 32-sample block of this wave
+    const int s_raw = blk * 32 + (lane & 31);
     const bool valid = s_raw < a.n;
     const int s = valid ? s_raw : a.n - 1;
     const float* P = a.packed;
     const float* H = a.packed + NR_F_HEAD;
-    const bool save = a.save != nullptr;
-    NrSave sv(a.save, a.n);
+    const int nb = (a.n + 31) / 32;
+    const bool save = a.save != nullptr && blk < nb;     // whole block, tail lanes included
+    float* const SV = a.save;
 
     // ---- point and direction ------------------------------------------------
     float px, py, pz, dx = 0.f, dy = 0.f, dz = 0.f;
@@ -187,22 +176,33 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         float pe[NR_PE_KSTEPS];
         if constexpr (EMB) pe_gather<15, NR_PE_KSTEPS>(pe, xrow, h);
         else pe_encode<15, NR_PE_KSTEPS>(pe, px, py, pz, h);
-        if (save && valid) {
-            float* row = sv.pe + (size_t)s * NR_SAVE_PE;
+        if (save) {
+            float* dst = SV + (size_t)blk * NR_NATIVE(64) + lane * 4;
 #pragma unroll
-            for (int g = 0; g < NR_PE_KSTEPS; ++g) row[2 * g + h] = pe[g];
+            for (int gq = 0; gq < NR_PE_KSTEPS / 4; ++gq) {
+                f32x4 v = {pe[4 * gq], pe[4 * gq + 1], pe[4 * gq + 2], pe[4 * gq + 3]};
+                *reinterpret_cast<f32x4*>(dst + gq * 256) = v;
+            }
         }
         init_bias<8>(A, H + NR_H_BIAS(1), h);
         mm_acc<NR_PE_KSTEPS, 8>(P + NR_F_L1, lane, A, [&](int g) { return pe[g]; });
         relu<8>(A);
     }
-    if (save && valid) store_rows<8>(A, sv.h[0] + (size_t)s * 256, h);
+    if (save) {
+        store_native<8>(A, SV + nr_sv_h(0, nb) + (size_t)blk * NR_NATIVE(256), lane);
+        store_mask<8>(A, (uint32_t*)(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + 0) * 256,
+                      lane);
+    }
 
 #define NR_DENSE(DST, SRC, LOFF, L)                                                   \
     init_bias<8>(DST, H + NR_H_BIAS(L), h);                                            \
     mm_acc<128, 8>(P + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; });   \
     relu<8>(DST);                                                                      \
-    if (save && valid) store_rows<8>(DST, sv.h[L - 1] + (size_t)s * 256, h);
+    if (save) {                                                                        \
+        store_native<8>(DST, SV + nr_sv_h(L - 1, nb) + (size_t)blk * NR_NATIVE(256), lane); \
+        store_mask<8>(DST, (uint32_t*)(SV + nr_sv_mask(nb)) +                          \
+                               ((size_t)blk * NR_MASK_LAYERS + L - 1) * 256, lane);    \
+    }
 
     NR_DENSE(B, A, NR_F_L2, 2)
     NR_DENSE(A, B, NR_F_L3, 3)
@@ -216,7 +216,11 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         mm_acc<128, 8>(P + NR_F_L5 + NR_PL(NR_PE_KSTEPS, 8), lane, A,
                        [&](int g) { return B[g >> 4][g & 15]; });
         relu<8>(A);
-        if (save && valid) store_rows<8>(A, sv.h[4] + (size_t)s * 256, h);
+        if (save) {
+            store_native<8>(A, SV + nr_sv_h(4, nb) + (size_t)blk * NR_NATIVE(256), lane);
+            store_mask<8>(A, (uint32_t*)(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + 4) * 256,
+                          lane);
+        }
     }
     NR_DENSE(B, A, NR_F_L6, 6)
     NR_DENSE(A, B, NR_F_L7, 7)
@@ -232,16 +236,19 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         // xyz_encoding_final: Linear(256,256), no activation (nerf.py:116)
         init_bias<8>(A, H + NR_H_BFINAL, h);
         mm_acc<128, 8>(P + NR_F_FINAL, lane, A, [&](int g) { return B[g >> 4][g & 15]; });
-        if (save && valid) store_rows<8>(A, sv.feat + (size_t)s * 256, h);
+        if (save) store_native<8>(A, SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256), lane);
 
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
         float dpe[NR_DIR_KSTEPS];
         if constexpr (EMB) pe_gather<6, NR_DIR_KSTEPS>(dpe, xrow + NR_XYZ_CH, h);
         else pe_encode<6, NR_DIR_KSTEPS>(dpe, dx, dy, dz, h);
-        if (save && valid) {
-            float* row = sv.dirpe + (size_t)s * NR_SAVE_DIR;
+        if (save) {
+            float* dst = SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32) + lane * 4;
 #pragma unroll
-            for (int g = 0; g < NR_DIR_KSTEPS; ++g) row[2 * g + h] = dpe[g];
+            for (int gq = 0; gq < NR_DIR_KSTEPS / 4; ++gq) {
+                f32x4 v = {dpe[4 * gq], dpe[4 * gq + 1], dpe[4 * gq + 2], dpe[4 * gq + 3]};
+                *reinterpret_cast<f32x4*>(dst + gq * 256) = v;
+            }
         }
         f32x16 C[4];
         init_bias<4>(C, H + NR_H_BDIR, h);
@@ -249,7 +256,11 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         mm_acc<NR_DIR_KSTEPS, 4>(P + NR_F_DIR + NR_PL(128, 4), lane, C,
                                  [&](int g) { return dpe[g]; });
         relu<4>(C);
-        if (save && valid) store_rows<4>(C, sv.hdir + (size_t)s * 128, h);
+        if (save) {
+            store_native<4>(C, SV + nr_sv_hdir(nb) + (size_t)blk * NR_NATIVE(128), lane);
+            store_mask<4>(C, (uint32_t*)(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + 8) * 256,
+                          lane);
+        }
 
         // rgb = Sigmoid(Linear(128,3)) (nerf.py:79-81,120)
         float rgb[3];

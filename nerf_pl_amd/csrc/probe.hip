@@ -7,8 +7,8 @@ NR_API int64_t nr_layout_query(int what) {
         case 0: return NR_F_TOTAL;
         case 1: return NR_F_HEAD;
         case 2: return NR_B_TOTAL;
-        case 3: return NR_SAVE_PER_SAMPLE;
-        case 4: return NR_GRAD_PER_SAMPLE;
+        case 3: return NR_SAVE_PER_BLOCK;
+        case 4: return NR_GRAD_PER_BLOCK;
         case 5: return NR_H_SIZE;
         case 6: return NR_F_L5;
         case 7: return NR_F_DIR;

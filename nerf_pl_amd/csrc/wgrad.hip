@@ -2,24 +2,26 @@
 // for every layer of NeRF (autograd of the nn.Linear layers, nerf.py:60-81).
 //
 // Grouped split-K GEMM on v_mfma_f32_32x32x2_f32.  Each of the 14 tasks
-// (dz segment x input segment, both row-major [n][width] as written by
-// mlp_fwd/mlp_bwd) is a <=256x256 output tile reduced over all n samples.  The
-// sample axis is split over the workgroups of a single, fully resident round
-// (grid <= 256 = one workgroup per CU), each task getting workgroups in
-// proportion to its cost.  A workgroup stages 16-sample slices of dz and x in
-// LDS (double buffered, coalesced float4 loads), its 4 waves each own a
-// 128x128 quadrant of the output, and it writes a partial slab; a second
-// kernel sums the slabs of each task in a fixed order (bitwise reproducible)
-// and scatters the result into the flat gradient buffer in
-// NeRF.named_parameters() order.
+// (a gradient segment dz x an input segment x, both in the block-native layout
+// of layout.h) is a <=256x256 output reduced over all samples.  Every task's
+// sample blocks are split over G_t workgroups (G_t proportional to its cost,
+// ~2 resident rounds in total).  A workgroup streams its blocks one 32-sample
+// block per stage into LDS, transposing the block-native chunks to
+// [sample][column] with ds_write_b128 (row stride 260: conflict-free), double
+// buffered; its 4 waves split the task's output with a per-task wave grid so
+// every SIMD holds MFMA work; k-step kk of a stage pairs samples 2kk and 2kk+1.
+// Each workgroup writes one partial slab; a second kernel sums a task's slabs
+// in a fixed order (bitwise reproducible) and scatters the result into the flat
+// gradient buffer in NeRF.named_parameters() order.
 #include "layout.h"
 
 namespace {
 
 constexpr int kTasks = 14;
-constexpr int kMaxWG = 256;
-constexpr int kSlab = 256 * 256 + 256;   // partial dW tile + partial bias
-constexpr int kTS = 16;                  // samples per LDS stage
+constexpr int kTargetWG = 480;   // ~2 rounds of one workgroup per CU
+constexpr int kRow = 260;        // LDS row stride (floats)
+
+enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
 
 // flat parameter offsets, NeRF.named_parameters() order (packing.py param_offsets)
 struct POff {
@@ -51,72 +53,90 @@ __device__ __forceinline__ int pe_feature(int g, int h, int np) {
     return -1;
 }
 
+struct WgSeg {
+    const float* base;   // segment start (block-native)
+    int kind, width;     // SegKind, columns
+};
+
 struct WgTask {
-    const float* dz; const float* x;
-    int dz_stride, x_stride, M, N;
+    WgSeg a, b;          // a = gradient (M = a.width), b = input (N = b.width)
+    int wm, wn;          // wave grid (wm * wn == 4)
+    int G;               // workgroups
+    int64_t slab;        // slab offset (floats) of workgroup 0
 };
 
 struct WgArgs {
     WgTask task[kTasks];
     int wg_start[kTasks + 1];
-    int n;
+    int nb, n;
     float* slab;
 };
 
-__device__ __forceinline__ int log2i(int v) { return 31 - __clz(v); }
+// float4 count of one block of a segment
+__device__ __forceinline__ int seg_f4(const WgSeg& s) {
+    return s.kind == SEG_ACC ? s.width * 8 : (s.kind == SEG_HEAD ? 32 : s.width * 8);
+}
+// (sample j, first column) of float4 e of a block
+__device__ __forceinline__ void seg_pos(int kind, int e, int& j, int& c) {
+    j = e & 31;
+    switch (kind) {
+        case SEG_ACC: c = 32 * (e >> 8) + 8 * ((e >> 6) & 3) + 4 * ((e >> 5) & 1); break;
+        case SEG_PE:  c = 32 * ((e >> 5) & 1) + 4 * (e >> 6); break;
+        case SEG_DPE: c = 16 * ((e >> 5) & 1) + 4 * (e >> 6); break;
+        default:      c = 0; j = e; break;
+    }
+}
 
-// Main loop of one workgroup; MT x NT = this wave's 32x32 tiles (compile
-// time, so accumulators stay in registers without per-MFMA branches).  Every
-// wave runs the same number of stages and barriers whatever its MT/NT.
 template <int MT, int NT>
-__device__ __forceinline__ void wgrad_body(const WgTask& T, int s0, int s1, int m0, int n0,
-                                           bool do_bias, float (*lds)[2][kTS][256],
-                                           float* __restrict__ slab) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int M4 = T.M >> 2, N4 = T.N >> 2;        // float4s per row (powers of 2)
-    const int lm = log2i(M4), ln = log2i(N4);
-    f32x16 acc[MT > 0 ? MT : 1][NT > 0 ? NT : 1];
+__device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int b0, int b1,
+                                           float* lds, float* __restrict__ slab) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int mi = wave / T.wn, ni = wave % T.wn;
+    const int m0 = 32 * MT * mi, n0 = 32 * NT * ni;
+    const int M = T.a.width, N = T.b.width;
+    const bool do_bias = ni == 0;
+    const int fa = seg_f4(T.a), fb = seg_f4(T.b);
+    const int blk_a = T.a.width * 32, blk_b = T.b.width * 32;   // floats per block
+
+    f32x16 acc[MT][NT];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x16{};
-    float bsum[MT > 0 ? MT : 1];
+    float bsum[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) bsum[i] = 0.f;
 
-    f32x4 ra[4], rb[4];
-    auto load = [&](int s) {
+    f32x4 ra[8], rb[8];
+    auto load = [&](int blk) {
+        const int nval = a.n - blk * 32;            // valid samples in this block
+        const f32x4* pa = reinterpret_cast<const f32x4*>(T.a.base + (size_t)blk * blk_a);
+        const f32x4* pb = reinterpret_cast<const f32x4*>(T.b.base + (size_t)blk * blk_b);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 8; ++i) {
             const int e = tid + 256 * i;
+            int j, c;
             ra[i] = f32x4{};
             rb[i] = f32x4{};
-            if (e < (kTS << lm)) {
-                const int r = e >> lm, q = e & (M4 - 1);
-                if (s + r < s1)
-                    ra[i] = *reinterpret_cast<const f32x4*>(T.dz + (size_t)(s + r) * T.dz_stride + 4 * q);
-            }
-            if (e < (kTS << ln)) {
-                const int r = e >> ln, q = e & (N4 - 1);
-                if (s + r < s1)
-                    rb[i] = *reinterpret_cast<const f32x4*>(T.x + (size_t)(s + r) * T.x_stride + 4 * q);
-            }
+            if (e < fa) { seg_pos(T.a.kind, e, j, c); if (j < nval) ra[i] = pa[e]; }
+            if (e < fb) { seg_pos(T.b.kind, e, j, c); if (j < nval) rb[i] = pb[e]; }
         }
     };
     auto store = [&](int buf) {
+        float* la = lds + buf * (2 * 32 * kRow);
+        float* lb = la + 32 * kRow;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 8; ++i) {
             const int e = tid + 256 * i;
-            if (e < (kTS << lm))
-                *reinterpret_cast<f32x4*>(&lds[buf][0][e >> lm][4 * (e & (M4 - 1))]) = ra[i];
-            if (e < (kTS << ln))
-                *reinterpret_cast<f32x4*>(&lds[buf][1][e >> ln][4 * (e & (N4 - 1))]) = rb[i];
+            int j, c;
+            if (e < fa) { seg_pos(T.a.kind, e, j, c); *reinterpret_cast<f32x4*>(la + j * kRow + c) = ra[i]; }
+            if (e < fb) { seg_pos(T.b.kind, e, j, c); *reinterpret_cast<f32x4*>(lb + j * kRow + c) = rb[i]; }
         }
     };
 
-    const int nst = (s1 - s0 + kTS - 1) / kTS;
+    const int nst = b1 - b0;
     if (nst > 0) {
-        load(s0);
+        load(b0);
         store(0);
     }
     __syncthreads();
@@ -124,87 +144,80 @@ __device__ __forceinline__ void wgrad_body(const WgTask& T, int s0, int s1, int 
 #pragma unroll 1
     for (int st = 0; st < nst; ++st) {
         const int buf = st & 1;
-        if (st + 1 < nst) load(s0 + (st + 1) * kTS);
-        if constexpr (MT > 0 && NT > 0) {
+        if (st + 1 < nst) load(b0 + st + 1);
+        const float* la = lds + buf * (2 * 32 * kRow);
+        const float* lb = la + 32 * kRow;
 #pragma unroll
-            for (int kk = 0; kk < kTS / 2; ++kk) {
-                const float* ar = &lds[buf][0][2 * kk + h][0];
-                const float* br = &lds[buf][1][2 * kk + h][0];
-                float av[MT], bv[NT];
+        for (int kk = 0; kk < 16; ++kk) {
+            const float* ar = la + (2 * kk + h) * kRow + m0 + col;
+            const float* br = lb + (2 * kk + h) * kRow + n0 + col;
+            float av[MT], bv[NT];
 #pragma unroll
-                for (int i = 0; i < MT; ++i) av[i] = ar[m0 + 32 * i + col];
+            for (int i = 0; i < MT; ++i) av[i] = ar[32 * i];
 #pragma unroll
-                for (int j = 0; j < NT; ++j) bv[j] = br[n0 + 32 * j + col];
+            for (int j = 0; j < NT; ++j) bv[j] = br[32 * j];
 #pragma unroll
-                for (int i = 0; i < MT; ++i)
+            for (int i = 0; i < MT; ++i)
 #pragma unroll
-                    for (int j = 0; j < NT; ++j) acc[i][j] = nr_mfma32(av[i], bv[j], acc[i][j]);
-                if (do_bias)
+                for (int j = 0; j < NT; ++j) acc[i][j] = nr_mfma32(av[i], bv[j], acc[i][j]);
+            if (do_bias)
 #pragma unroll
-                    for (int i = 0; i < MT; ++i) bsum[i] += av[i];
-            }
+                for (int i = 0; i < MT; ++i) bsum[i] += av[i];
         }
         if (st + 1 < nst) store(buf ^ 1);
         __syncthreads();
     }
-    if constexpr (MT > 0 && NT > 0) {
 #pragma unroll
-        for (int i = 0; i < MT; ++i) {
+    for (int i = 0; i < MT; ++i) {
 #pragma unroll
-            for (int j = 0; j < NT; ++j)
+        for (int j = 0; j < NT; ++j)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int o = m0 + 32 * i + nr_acc_row(r, h);
-                    slab[o * 256 + n0 + 32 * j + col] = acc[i][j][r];
-                }
-            if (do_bias) {
-                const float b = bsum[i] + __shfl_xor(bsum[i], 32);
-                if (h == 0) slab[256 * 256 + m0 + 32 * i + col] = b;
+            for (int r = 0; r < 16; ++r) {
+                const int o = m0 + 32 * i + nr_acc_row(r, h);
+                const int c = n0 + 32 * j + col;
+                if (o < M && c < N) slab[o * N + c] = acc[i][j][r];
             }
+        if (do_bias) {
+            const float b = bsum[i] + __shfl_xor(bsum[i], 32);
+            const int o = m0 + 32 * i + col;
+            if (h == 0 && o < M) slab[M * N + o] = b;
         }
     }
 }
 
 __global__ void __launch_bounds__(256, 1) wgrad_kernel(WgArgs a) {
-    __shared__ float lds[2][2][kTS][256];   // [buf][A|B][sample][col]  64 KiB
+    __shared__ __attribute__((aligned(16))) float lds[2 * 2 * 32 * kRow];   // 130 KiB
     int t = 0;
 #pragma unroll 1
     while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
-    const WgTask T = a.task[t];
-    const int G = a.wg_start[t + 1] - a.wg_start[t];
+    const WgTask& T = a.task[t];
     const int c = blockIdx.x - a.wg_start[t];
-    const int nblk = (a.n + kTS - 1) / kTS;
-    const int s0 = (int)((int64_t)c * nblk / G) * kTS;
-    const int s1 = min((int)((int64_t)(c + 1) * nblk / G) * kTS, a.n);
-    const int wave = threadIdx.x >> 6;
-    const int m0 = 128 * (wave >> 1), n0 = 128 * (wave & 1);
-    const int mtc = max(0, min(4, (T.M - m0 + 31) / 32));
-    const int ntc = max(0, min(4, (T.N - n0 + 31) / 32));
-    const bool do_bias = (wave & 1) == 0;
-    float* slab = a.slab + (size_t)blockIdx.x * kSlab;
-    // wave-uniform dispatch on this wave's tile counts (the shapes of the 14 tasks)
-    const int key = __builtin_amdgcn_readfirstlane(mtc * 8 + ntc);
+    const int b0 = (int)((int64_t)c * a.nb / T.G);
+    const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
+    float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
+    const int M = T.a.width, N = T.b.width;
+    const int key = __builtin_amdgcn_readfirstlane(((M / T.wm + 31) / 32) * 8 + (N / T.wn + 31) / 32);
     switch (key) {
-        case 4 * 8 + 4: wgrad_body<4, 4>(T, s0, s1, m0, n0, do_bias, lds, slab); break;
-        case 4 * 8 + 2: wgrad_body<4, 2>(T, s0, s1, m0, n0, do_bias, lds, slab); break;
-        case 4 * 8 + 1: wgrad_body<4, 1>(T, s0, s1, m0, n0, do_bias, lds, slab); break;
-        case 1 * 8 + 4: wgrad_body<1, 4>(T, s0, s1, m0, n0, do_bias, lds, slab); break;
-        default: wgrad_body<0, 0>(T, s0, s1, m0, n0, do_bias, lds, slab); break;
+        case 4 * 8 + 4: wgrad_body<4, 4>(a, T, b0, b1, lds, slab); break;
+        case 2 * 8 + 4: wgrad_body<2, 4>(a, T, b0, b1, lds, slab); break;
+        case 2 * 8 + 2: wgrad_body<2, 2>(a, T, b0, b1, lds, slab); break;
+        case 1 * 8 + 2: wgrad_body<1, 2>(a, T, b0, b1, lds, slab); break;
+        default:        wgrad_body<1, 1>(a, T, b0, b1, lds, slab); break;
     }
 }
 
 // destination of output element (o, c) of task t in the flat gradient (-1 = none)
 __device__ int wgrad_dest(int t, int o, int c) {
     switch (t) {
-        case 0: { const int f = pe_feature(c >> 1, c & 1, 15);
+        case 0: { const int f = pe_feature(c & 31, c >> 5, 15);
                   return f < 0 ? -1 : kP.w[0] + o * kP.fan[0] + f; }
         case 1: case 2: case 3: return kP.w[t] + o * kP.fan[t] + c;
-        case 4: { const int f = pe_feature(c >> 1, c & 1, 15);
+        case 4: { const int f = pe_feature(c & 31, c >> 5, 15);
                   return f < 0 ? -1 : kP.w[4] + o * kP.fan[4] + f; }
         case 5: return kP.w[4] + o * kP.fan[4] + NR_XYZ_CH + c;
         case 6: case 7: case 8: case 9: return kP.w[t - 1] + o * kP.fan[t - 1] + c;
         case 10: return kP.w[9] + o * kP.fan[9] + c;
-        case 11: { const int f = pe_feature(c >> 1, c & 1, 6);
+        case 11: { const int f = pe_feature(c & 15, c >> 4, 6);
                    return f < 0 ? -1 : kP.w[9] + o * kP.fan[9] + 256 + f; }
         case 12: return o == 3 ? kP.w[10] + c : -1;
         case 13: return o < 3 ? kP.w[11] + o * kP.fan[11] + c : -1;
@@ -226,44 +239,25 @@ __device__ int wgrad_bias_dest(int t, int o) {
 
 __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
     const int t = blockIdx.y;
-    const WgTask T = a.task[t];
+    const WgTask& T = a.task[t];
+    const int M = T.a.width, N = T.b.width;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nw = T.M * T.N;
-    if (e >= nw + T.M) return;
-    int off, dst;
-    if (e < nw) {
-        const int o = e / T.N, c = e % T.N;
-        off = o * 256 + c;
-        dst = wgrad_dest(t, o, c);
-    } else {
-        const int o = e - nw;
-        off = 256 * 256 + o;
-        dst = wgrad_bias_dest(t, o);
-    }
+    const int nw = M * N, sz = nw + M;
+    if (e >= sz) return;
+    const int dst = e < nw ? wgrad_dest(t, e / N, e % N) : wgrad_bias_dest(t, e - nw);
     if (dst < 0) return;
-    const float* p = a.slab + (size_t)a.wg_start[t] * kSlab + off;
+    const float* p = a.slab + T.slab + e;
     float s = 0.f;
-    for (int w = a.wg_start[t]; w < a.wg_start[t + 1]; ++w, p += kSlab) s += *p;
+    for (int w = 0; w < T.G; ++w, p += sz) s += *p;
     grad[dst] = s;
-}
-
-// per-sample cost of a task for its busiest wave (MFMA tile pairs)
-int task_cost(int M, int N) {
-    int best = 0;
-    for (int w = 0; w < 4; ++w) {
-        const int m0 = 128 * (w >> 1), n0 = 128 * (w & 1);
-        const int mt = std::max(0, std::min(4, (M - m0 + 31) / 32));
-        const int nt = std::max(0, std::min(4, (N - n0 + 31) / 32));
-        best = std::max(best, mt * nt);
-    }
-    return best;
 }
 
 }  // namespace
 
 NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
     (void)n;
-    return (int64_t)kMaxWG * kSlab * sizeof(float);
+    // upper bound of sum_t G_t * (M_t N_t + M_t) for the task list below
+    return (int64_t)(kTargetWG + kTasks) * (256 * 256 + 256) * sizeof(float);
 }
 
 NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
@@ -278,44 +272,46 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
         if (e != hipSuccess) { nr_set_error("nr_wgrad: memset failed"); return (int)e; }
         return 0;
     }
-    NrSave sv(const_cast<float*>(save), n);
-    NrGrad gd(const_cast<float*>(grad_ws), n);
-    WgArgs a{};
+    const int64_t nb = (n + 31) / 32;
+    float* SV = const_cast<float*>(save);
+    float* GD = const_cast<float*>(grad_ws);
+    auto acc = [](float* p, int w) { return WgSeg{p, SEG_ACC, w}; };
+    const WgSeg pe{SV, SEG_PE, 64}, dpe{SV + nr_sv_dirpe(nb), SEG_DPE, 32};
+    const WgSeg head{GD + nr_gd_dhead(nb), SEG_HEAD, 4};
+    auto H = [&](int l) { return acc(SV + nr_sv_h(l, nb), 256); };
+    auto DZ = [&](int l) { return acc(GD + nr_gd_dz(l, nb), 256); };
+    const WgSeg feat = acc(SV + nr_sv_feat(nb), 256), hdir = acc(SV + nr_sv_hdir(nb), 128);
+    const WgSeg dzdir = acc(GD + nr_gd_dzdir(nb), 128);
+    // (a, b, wm, wn); task order fixes wgrad_dest / wgrad_bias_dest
     const WgTask tasks[kTasks] = {
-        {gd.dz[0], sv.pe, 256, 64, 256, 64},
-        {gd.dz[1], sv.h[0], 256, 256, 256, 256},
-        {gd.dz[2], sv.h[1], 256, 256, 256, 256},
-        {gd.dz[3], sv.h[2], 256, 256, 256, 256},
-        {gd.dz[4], sv.pe, 256, 64, 256, 64},
-        {gd.dz[4], sv.h[3], 256, 256, 256, 256},
-        {gd.dz[5], sv.h[4], 256, 256, 256, 256},
-        {gd.dz[6], sv.h[5], 256, 256, 256, 256},
-        {gd.dz[7], sv.h[6], 256, 256, 256, 256},
-        {gd.dfeat, sv.h[7], 256, 256, 256, 256},
-        {gd.dzdir, sv.feat, 128, 256, 128, 256},
-        {gd.dzdir, sv.dirpe, 128, 32, 128, 32},
-        {gd.dhead, sv.h[7], 4, 256, 4, 256},
-        {gd.dhead, sv.hdir, 4, 128, 4, 128},
+        {DZ(0), pe, 4, 1}, {DZ(1), H(0), 2, 2}, {DZ(2), H(1), 2, 2}, {DZ(3), H(2), 2, 2},
+        {DZ(4), pe, 4, 1}, {DZ(4), H(3), 2, 2}, {DZ(5), H(4), 2, 2}, {DZ(6), H(5), 2, 2},
+        {DZ(7), H(6), 2, 2}, {DZ(8), H(7), 2, 2}, {dzdir, feat, 2, 2}, {dzdir, dpe, 4, 1},
+        {head, H(7), 1, 4}, {head, hdir, 1, 4},
     };
+    WgArgs a{};
     int cost[kTasks], tot = 0;
     for (int t = 0; t < kTasks; ++t) {
         a.task[t] = tasks[t];
-        cost[t] = task_cost(tasks[t].M, tasks[t].N);
+        const int mt = (tasks[t].a.width / tasks[t].wm + 31) / 32;
+        const int nt = (tasks[t].b.width / tasks[t].wn + 31) / 32;
+        cost[t] = mt * nt;   // MFMAs per k-step of each (equally loaded) wave
         tot += cost[t];
     }
-    // one resident round: floor share of 256 workgroups, at least one each,
-    // and no more workgroups than 16-sample stages
-    const int nblk = (int)((n + kTS - 1) / kTS);
     a.wg_start[0] = 0;
+    int64_t slab = 0;
     for (int t = 0; t < kTasks; ++t) {
-        int g = std::max(1, (kMaxWG - kTasks) * cost[t] / tot);
-        g = std::min(g, nblk);
-        a.wg_start[t + 1] = a.wg_start[t] + g;
+        int64_t g = (kTargetWG * cost[t] + tot - 1) / tot;   // per-workgroup work <= target
+        g = std::max<int64_t>(1, std::min<int64_t>(g, nb));
+        a.task[t].G = (int)g;
+        a.task[t].slab = slab;
+        slab += (int64_t)g * (tasks[t].a.width * tasks[t].b.width + tasks[t].a.width);
+        a.wg_start[t + 1] = a.wg_start[t] + (int)g;
     }
+    a.nb = (int)nb;
     a.n = (int)n;
     a.slab = workspace;
-    const int nwg = a.wg_start[kTasks];
-    wgrad_kernel<<<nwg, 256, 0, st>>>(a);
+    wgrad_kernel<<<a.wg_start[kTasks], 256, 0, st>>>(a);
     NR_LAUNCH_CHECK("nr_wgrad");
     dim3 rg((256 * 256 + 256 + 255) / 256, kTasks);
     wgrad_reduce_kernel<<<rg, 256, 0, st>>>(a, grad_flat);

@@ -59,7 +59,7 @@ class _FusedMLP(torch.autograd.Function):
             g4 = torch.zeros(n, 4, device=dev)
             g4[:, 3:4] = g_out
             g_out = g4
-        grad_ws = torch.empty(n * ops.GRAD_PER_SAMPLE, device=dev)
+        grad_ws = torch.empty(ops.n_blocks(n) * ops.GRAD_PER_BLOCK, device=dev)
         g_out = g_out.contiguous()
         call("nr_mlp_bwd", packed_b.data_ptr(), packed_f.data_ptr(), out.data_ptr(),
              g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), stream_of(dev))

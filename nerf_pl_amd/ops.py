@@ -14,8 +14,14 @@ import torch
 from . import packing
 from ._lib import call, lib, ptr, stream_of
 
-SAVE_PER_SAMPLE = 64 + 8 * 256 + 256 + 128 + 32        # csrc/layout.h NR_SAVE_PER_SAMPLE
-GRAD_PER_SAMPLE = 8 * 256 + 256 + 128 + 4              # NR_GRAD_PER_SAMPLE
+BLK = 32                                                # samples per block (one wave)
+# csrc/layout.h NR_SAVE_PER_BLOCK / NR_GRAD_PER_BLOCK (block-native layout)
+SAVE_PER_BLOCK = BLK * (64 + 8 * 256 + 256 + 128 + 32) + 9 * 256
+GRAD_PER_BLOCK = BLK * (9 * 256 + 128 + 4)
+
+
+def n_blocks(n: int) -> int:
+    return (n + BLK - 1) // BLK
 FWD_PACKED = packing.layer_offsets(packing.FWD_LAYERS)[1] + packing.HEAD_SIZE
 BWD_PACKED = packing.layer_offsets(packing.BWD_LAYERS)[1]
 
@@ -76,7 +82,7 @@ def mlp_forward(packed: torch.Tensor, *, rays=None, z=None, samples_per_ray=0, x
         n, xstride = z.numel(), 0
     dev = packed.device
     out = torch.empty(n, 1 if sigma_only else 4, device=dev)
-    sv = torch.empty(n * SAVE_PER_SAMPLE, device=dev) if save else None
+    sv = torch.empty(n_blocks(n) * SAVE_PER_BLOCK, device=dev) if save else None
     call("nr_mlp_fwd", ptr(packed), ptr(rays), ptr(z), n, int(samples_per_ray), ptr(x), xstride,
          int(sigma_only), ptr(out), ptr(sv), stream_of(dev))
     return out, sv
@@ -152,6 +158,34 @@ def probe_mfma32(a, b):
 
 def layout_query(what: int) -> int:
     return int(lib().nr_layout_query(what))
+
+
+def native_to_rows(seg: torch.Tensor, n: int, width: int) -> torch.Tensor:
+    """Decode a block-native activation segment (layout.h) to (n, width) rows:
+    element [block][t][q][lane=32h+j][e] is feature 32t+8q+4h+e of sample j."""
+    nb = n_blocks(n)
+    x = seg[: nb * BLK * width].view(nb, width // 32, 4, 2, BLK, 4)
+    return x.permute(0, 4, 1, 2, 3, 5).reshape(nb * BLK, width)[:n]
+
+
+def pe_to_rows(seg: torch.Tensor, n: int, ksteps: int) -> torch.Tensor:
+    """Decode a PE segment [block][g/4][lane][g%4] to (n, 2*ksteps) rows with
+    column 32h+g (xyz, ksteps=32) / 16h+g (dir, ksteps=16) = pe value (g, h)."""
+    nb = n_blocks(n)
+    x = seg[: nb * BLK * 2 * ksteps].view(nb, ksteps // 4, 2, BLK, 4)
+    return x.permute(0, 3, 2, 1, 4).reshape(nb * BLK, 2 * ksteps)[:n]
+
+
+def save_segments(sv: torch.Tensor, n: int) -> dict:
+    """Named views of a training save buffer (csrc/layout.h NrSave order)."""
+    nb = n_blocks(n)
+    o, out = 0, {}
+    for name, w in [("pe", 64)] + [(f"h{i}", 256) for i in range(1, 9)] + \
+                   [("feat", 256), ("hdir", 128), ("dirpe", 32)]:
+        out[name] = sv[o:o + nb * BLK * w]
+        o += nb * BLK * w
+    out["mask"] = sv[o:o + nb * 9 * 256]
+    return out
 
 
 def np_maps():

@@ -1,0 +1,69 @@
+"""Isolated timing of the fused MLP kernels at the cfg2 fine-pass size
+(786,432 samples), for profiling (dev tool).  Usage: kbench.py [fwd|fwdsave|bwd|wgrad|all] [reps]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from nerf_pl_amd import ops, packing
+from nerf_pl_amd._lib import call, stream_of
+from nerf_pl_amd.functions import _wgrad_workspace
+
+FLOP = {"fwd": 1186816, "fwdsave": 1186816, "bwd": 1115392, "wgrad": 1186816}
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    flat = (torch.rand(packing.N_PARAMS, device=dev) - 0.5) * 0.15
+    pf, pb = ops.pack_fwd(flat), ops.pack_bwd(flat)
+    n_rays, spr = 4096, 192
+    n = n_rays * spr
+    rays = torch.randn(n_rays, 8, device=dev)
+    rays[:, 3:6] = torch.nn.functional.normalize(rays[:, 3:6], dim=-1)
+    rays[:, 6], rays[:, 7] = 2.0, 6.0
+    z = (torch.rand(n, device=dev) * 4 + 2).contiguous()
+    out, sv = ops.mlp_forward(pf, rays=rays, z=z, samples_per_ray=spr, save=True)
+    gout = torch.randn(n, 4, device=dev)
+    gw = torch.empty(ops.n_blocks(n) * ops.GRAD_PER_BLOCK, device=dev)
+    ws = _wgrad_workspace(0)
+    gflat = torch.empty(packing.N_PARAMS, device=dev)
+    st = stream_of(dev)
+
+    def run(k):
+        if k == "fwd":
+            call("nr_mlp_fwd", pf.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0,
+                 out.data_ptr(), None, st)
+        elif k == "fwdsave":
+            call("nr_mlp_fwd", pf.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0,
+                 out.data_ptr(), sv.data_ptr(), st)
+        elif k == "bwd":
+            call("nr_mlp_bwd", pb.data_ptr(), pf.data_ptr(), out.data_ptr(), gout.data_ptr(),
+                 sv.data_ptr(), n, gw.data_ptr(), st)
+        elif k == "wgrad":
+            call("nr_wgrad", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
+
+    ks = ["fwd", "fwdsave", "bwd", "wgrad"] if which == "all" else [which]
+    run("bwd")
+    for k in ks:
+        for _ in range(2):
+            run(k)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run(k)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        tf = n * FLOP[k] / (ms * 1e-3) / 1e12
+        print(f"{k:8s} {ms:8.3f} ms  {tf:6.1f} TFLOP/s  {tf / 157.3 * 100:5.1f}% of fp32 MFMA peak",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -31,8 +31,8 @@ def test_layout_constants_match_packing():
     assert ops.layout_query(0) == ftot + packing.HEAD_SIZE == ops.FWD_PACKED
     assert ops.layout_query(1) == ftot
     assert ops.layout_query(2) == btot == ops.BWD_PACKED
-    assert ops.layout_query(3) == ops.SAVE_PER_SAMPLE
-    assert ops.layout_query(4) == ops.GRAD_PER_SAMPLE
+    assert ops.layout_query(3) == ops.SAVE_PER_BLOCK
+    assert ops.layout_query(4) == ops.GRAD_PER_BLOCK
     assert ops.layout_query(5) == packing.HEAD_SIZE
     assert ops.layout_query(6) == fo["L5"]
     assert ops.layout_query(7) == fo["dir"]

@@ -125,31 +125,45 @@ def test_mlp_forward_saved_activations():
     hdir = torch.relu(torch.nn.functional.linear(torch.cat([feat, e_dir], -1),
                                                  p["dir_encoding.0.weight"],
                                                  p["dir_encoding.0.bias"]))
-    o = 0
-    pe = sv[o:o + 64 * n].view(n, 64); o += 64 * n
+    seg = ops.save_segments(sv, n)
+    pe = ops.pe_to_rows(seg["pe"], n, 32)
     pm = packing.PE_MAP
     for g_ in range(32):
         for hh in range(2):
             f = pm[g_, hh]
-            col = pe[:, 2 * g_ + hh]
+            col = pe[:, 32 * hh + g_]
             if f < 0:
                 assert torch.all(col == 0)
             else:
                 torch.testing.assert_close(col, e_xyz[:, f], rtol=0, atol=2e-6)
     for l in range(8):
-        got = sv[o:o + 256 * n].view(n, 256); o += 256 * n
+        got = ops.native_to_rows(seg[f"h{l+1}"], n, 256)
         assert (got - hs[l]).abs().max().item() < 2e-5, f"h{l+1}"
-    got = sv[o:o + 256 * n].view(n, 256); o += 256 * n
+    got = ops.native_to_rows(seg["feat"], n, 256)
     assert (got - feat).abs().max().item() < 2e-5
-    got = sv[o:o + 128 * n].view(n, 128); o += 128 * n
+    got = ops.native_to_rows(seg["hdir"], n, 128)
     assert (got - hdir).abs().max().item() < 2e-5
-    dpe = sv[o:o + 32 * n].view(n, 32)
+    dpe = ops.pe_to_rows(seg["dirpe"], n, 16)
     dm = packing.DIR_MAP
     for g_ in range(16):
         for hh in range(2):
             f = dm[g_, hh]
             if f >= 0:
-                torch.testing.assert_close(dpe[:, 2 * g_ + hh], e_dir[:, f], rtol=0, atol=2e-6)
+                torch.testing.assert_close(dpe[:, 16 * hh + g_], e_dir[:, f], rtol=0, atol=2e-6)
+    # ReLU bit masks: bit (16*(t&1)+r) of word t>>1 of lane l <-> activation > 0
+    nb = ops.n_blocks(n)
+    words = seg["mask"].view(torch.int32).view(nb, 9, 64, 4).numpy().astype(np.uint32)
+    for l, act in list(enumerate(hs)) + [(8, hdir)]:
+        nt = act.shape[1] // 32
+        for s_ in range(0, n, 7):
+            b_, j = divmod(s_, 32)
+            for hh in range(2):
+                w4 = words[b_, l, 32 * hh + j]
+                for t in range(nt):
+                    for r in range(16):
+                        f = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh
+                        bit = (w4[t >> 1] >> (16 * (t & 1) + r)) & 1
+                        assert bit == int(act[s_, f] > 0), (l, s_, f)
 
 
 @pytest.mark.parametrize("case", ["cfg2_n26", "cfg2_n1200", "disp_chunk", "ragged", "cfg1_s32"])
