@@ -107,6 +107,59 @@ __host__ __device__ __forceinline__ int64_t nr_gd_dhead(int64_t nb) {
 }
 
 // wave-level helpers shared by the fused kernels ---------------------------
+// Fused-MLP layer: acc[t] += sum_g Wpacked[g][t] * B(g), g in [0, KS).
+// Weights stream as one float4 wave load per (4 k-steps x tile), double
+// buffered one group ahead.  side(grp) runs right after the prefetch of each
+// group is issued: the kernels use it to spread the previous layer's output
+// stores over this layer, so that no weight-load wait (vmcnt counts stores and
+// loads together, in issue order) sits behind a burst of stores.
+template <int NT>
+__device__ __forceinline__ void nr_ld_wgrp(const float* __restrict__ w, int grp, int lane,
+                                           f32x4 (&dst)[NT]) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(w) + (size_t)grp * NT * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) dst[t] = p[t * 64];
+}
+
+struct NrNoSide {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <int KS, int NT, typename GetB, typename Side = NrNoSide>
+__device__ __forceinline__ void nr_mm_acc(const float* __restrict__ w, int lane, f32x16 (&acc)[NT],
+                                          GetB getb, Side side = Side()) {
+    static_assert(KS % 8 == 0, "k-steps must be a multiple of 8");
+    f32x4 wa[NT], wb[NT];
+    nr_ld_wgrp<NT>(w, 0, lane, wa);
+#pragma unroll
+    for (int grp = 0; grp < KS / 4; grp += 2) {
+        nr_ld_wgrp<NT>(w, grp + 1, lane, wb);
+        side(grp);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const float b = getb(grp * 4 + kk);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wa[t][kk], b, acc[t]);
+        }
+        if (grp + 2 < KS / 4) nr_ld_wgrp<NT>(w, grp + 2, lane, wa);
+        side(grp + 1);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const float b = getb(grp * 4 + 4 + kk);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wb[t][kk], b, acc[t]);
+        }
+    }
+}
+
+// piece p (= 4t + q) of a block-native store: one float4 per lane
+template <int NT>
+__device__ __forceinline__ void store_native_piece(const f32x16 (&acc)[NT], int p,
+                                                   float* __restrict__ blk, int lane) {
+    const int t = p >> 2, q = p & 3;
+    f32x4 v = {acc[t][4 * q + 0], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+    *reinterpret_cast<f32x4*>(blk + (p * 64 + lane) * 4) = v;
+}
 template <int NT>
 __device__ __forceinline__ void store_native(const f32x16 (&acc)[NT], float* __restrict__ blk,
                                              int lane) {

@@ -13,39 +13,6 @@ namespace {
 constexpr int kWaves = 4;
 
 template <int NT>
-__device__ __forceinline__ void ld_wgrp(const float* __restrict__ w, int grp, int lane,
-                                        f32x4 (&dst)[NT]) {
-    const f32x4* p = reinterpret_cast<const f32x4*>(w) + (size_t)grp * NT * 64 + lane;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) dst[t] = p[t * 64];
-}
-
-template <int KS, int NT, typename GetB>
-__device__ __forceinline__ void mm_acc(const float* __restrict__ w, int lane, f32x16 (&acc)[NT],
-                                       GetB getb) {
-    static_assert(KS % 8 == 0, "k-steps must be a multiple of 8");
-    f32x4 wa[NT], wb[NT];
-    ld_wgrp<NT>(w, 0, lane, wa);
-#pragma unroll
-    for (int grp = 0; grp < KS / 4; grp += 2) {
-        ld_wgrp<NT>(w, grp + 1, lane, wb);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const float b = getb(grp * 4 + kk);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wa[t][kk], b, acc[t]);
-        }
-        if (grp + 2 < KS / 4) ld_wgrp<NT>(w, grp + 2, lane, wa);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const float b = getb(grp * 4 + 4 + kk);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wb[t][kk], b, acc[t]);
-        }
-    }
-}
-
-template <int NT>
 __device__ __forceinline__ void zero(f32x16 (&acc)[NT]) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
@@ -119,16 +86,23 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
                     C[t][4 * q + e] = nr_mask_bit(d, mw[t >> 1], 16 * (t & 1) + 4 * q + e);
                 }
             }
-        store_native<4>(C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_NATIVE(128), lane);
     }
 
     f32x16 A[8], B[8];
-    // d feat = W_dir[:, :256]^T dz_dir   (xyz_encoding_final has no activation)
+    // each layer's dz is written while the next backward layer runs (side hook)
+    auto dzseg = [&](int l) { return GD + nr_gd_dz(l, nb) + (size_t)blk * NR_NATIVE(256); };
+    auto side8 = [&](const f32x16 (&X)[8], float* dst) {
+        return [&X, dst, lane](int grp) { if (grp < 32) store_native_piece<8>(X, grp, dst, lane); };
+    };
+    // d feat = W_dir[:, :256]^T dz_dir   (xyz_encoding_final has no activation); stores dz_dir
     zero<8>(A);
-    mm_acc<64, 8>(PB + NR_B_DIRT, lane, A, [&](int g) { return C[g >> 4][g & 15]; });
-    store_native<8>(A, GD + nr_gd_dz(8, nb) + (size_t)blk * NR_NATIVE(256), lane);
+    {
+        float* cdst = GD + nr_gd_dzdir(nb) + (size_t)blk * NR_NATIVE(128);
+        nr_mm_acc<64, 8>(PB + NR_B_DIRT, lane, A, [&](int g) { return C[g >> 4][g & 15]; },
+                         [&](int grp) { store_native_piece<4>(C, grp, cdst, lane); });
+    }
 
-    // d h8 = W_final^T dfeat + W_sigma^T dsigma, masked by h8
+    // d h8 = W_final^T dfeat + W_sigma^T dsigma, masked by h8; stores dfeat
 #pragma unroll
     for (int t = 0; t < 8; ++t)
 #pragma unroll
@@ -139,28 +113,29 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
         }
     {
         const uint4 mk = mask[7 * 64];
-        mm_acc<128, 8>(PB + NR_B_FINALT, lane, B, [&](int g) { return A[g >> 4][g & 15]; });
+        nr_mm_acc<128, 8>(PB + NR_B_FINALT, lane, B, [&](int g) { return A[g >> 4][g & 15]; },
+                          side8(A, dzseg(8)));
         relu_mask<8>(B, mk);
-        store_native<8>(B, GD + nr_gd_dz(7, nb) + (size_t)blk * NR_NATIVE(256), lane);
     }
 
-#define NR_BACK(DST, SRC, LOFF, L)                                                          \
-    {                                                                                        \
-        const uint4 mk = mask[(L - 1) * 64];                                                 \
-        zero<8>(DST);                                                                        \
-        mm_acc<128, 8>(PB + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; });    \
-        relu_mask<8>(DST, mk);                                                               \
-        store_native<8>(DST, GD + nr_gd_dz(L - 1, nb) + (size_t)blk * NR_NATIVE(256), lane); \
+#define NR_BACK(DST, SRC, LOFF, L)                                                           \
+    {                                                                                         \
+        const uint4 mk = mask[(L - 1) * 64];                                                  \
+        zero<8>(DST);                                                                         \
+        nr_mm_acc<128, 8>(PB + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; },   \
+                          side8(SRC, dzseg(L)));                                              \
+        relu_mask<8>(DST, mk);                                                                \
     }
 
-    NR_BACK(A, B, NR_B_L8T, 7)   // dz7 = (W8^T dz8) * [h7 > 0]
+    NR_BACK(A, B, NR_B_L8T, 7)   // dz7 = (W8^T dz8) * [h7 > 0], stores dz8
     NR_BACK(B, A, NR_B_L7T, 6)
     NR_BACK(A, B, NR_B_L6T, 5)
     NR_BACK(B, A, NR_B_L5T, 4)   // through the h4 columns of the skip layer
     NR_BACK(A, B, NR_B_L4T, 3)
     NR_BACK(B, A, NR_B_L3T, 2)
-    NR_BACK(A, B, NR_B_L2T, 1)
+    NR_BACK(A, B, NR_B_L2T, 1)   // stores dz2, leaves dz1 in A
 #undef NR_BACK
+    store_native<8>(A, dzseg(0), lane);
 }
 
 }  // namespace

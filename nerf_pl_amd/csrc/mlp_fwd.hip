@@ -16,41 +16,6 @@ namespace {
 constexpr int kWaves = 4;   // waves per workgroup (one per SIMD)
 
 template <int NT>
-__device__ __forceinline__ void ld_wgrp(const float* __restrict__ w, int grp, int lane,
-                                        f32x4 (&dst)[NT]) {
-    const f32x4* p = reinterpret_cast<const f32x4*>(w) + (size_t)grp * NT * 64 + lane;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) dst[t] = p[t * 64];
-}
-
-// acc[t] += sum_g Wpacked[g][t] * B(g), g in [0, KS).  getb(g) must fold to a
-// register for compile-time g.
-template <int KS, int NT, typename GetB>
-__device__ __forceinline__ void mm_acc(const float* __restrict__ w, int lane, f32x16 (&acc)[NT],
-                                       GetB getb) {
-    static_assert(KS % 8 == 0, "k-steps must be a multiple of 8");
-    f32x4 wa[NT], wb[NT];
-    ld_wgrp<NT>(w, 0, lane, wa);
-#pragma unroll
-    for (int grp = 0; grp < KS / 4; grp += 2) {
-        ld_wgrp<NT>(w, grp + 1, lane, wb);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const float b = getb(grp * 4 + kk);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wa[t][kk], b, acc[t]);
-        }
-        if (grp + 2 < KS / 4) ld_wgrp<NT>(w, grp + 2, lane, wa);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const float b = getb(grp * 4 + 4 + kk);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wb[t][kk], b, acc[t]);
-        }
-    }
-}
-
-template <int NT>
 __device__ __forceinline__ void init_bias(f32x16 (&acc)[NT], const float* __restrict__ b, int h) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -172,39 +137,42 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     }
 
     f32x16 A[8], B[8];
+    // Saved-activation stores (training): each layer's output is written while
+    // the next layer runs (nr_mm_acc side hook), one float4 per weight group.
+    auto hseg = [&](int l) { return SV + nr_sv_h(l, nb) + (size_t)blk * NR_NATIVE(256); };
+    auto mseg = [&](int l) {
+        return reinterpret_cast<uint32_t*>(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + l) * 256;
+    };
+    auto side_acc8 = [&](const f32x16 (&X)[8], float* dst, uint32_t* msk) {
+        return [&X, dst, msk, save, lane](int grp) {
+            if (!save) return;
+            if (grp < 32) store_native_piece<8>(X, grp, dst, lane);
+            if (grp == 0 && msk) store_mask<8>(X, msk, lane);
+        };
+    };
     {   // layer 1: PE(63) -> 256
         float pe[NR_PE_KSTEPS];
         if constexpr (EMB) pe_gather<15, NR_PE_KSTEPS>(pe, xrow, h);
         else pe_encode<15, NR_PE_KSTEPS>(pe, px, py, pz, h);
-        if (save) {
-            float* dst = SV + (size_t)blk * NR_NATIVE(64) + lane * 4;
-#pragma unroll
-            for (int gq = 0; gq < NR_PE_KSTEPS / 4; ++gq) {
-                f32x4 v = {pe[4 * gq], pe[4 * gq + 1], pe[4 * gq + 2], pe[4 * gq + 3]};
-                *reinterpret_cast<f32x4*>(dst + gq * 256) = v;
-            }
-        }
+        float* pdst = SV + (size_t)blk * NR_NATIVE(64);
         init_bias<8>(A, H + NR_H_BIAS(1), h);
-        mm_acc<NR_PE_KSTEPS, 8>(P + NR_F_L1, lane, A, [&](int g) { return pe[g]; });
+        nr_mm_acc<NR_PE_KSTEPS, 8>(P + NR_F_L1, lane, A, [&](int g) { return pe[g]; },
+                                   [&](int grp) {
+                                       if (!save) return;
+                                       f32x4 v = {pe[4 * grp], pe[4 * grp + 1], pe[4 * grp + 2],
+                                                  pe[4 * grp + 3]};
+                                       *reinterpret_cast<f32x4*>(pdst + (grp * 64 + lane) * 4) = v;
+                                   });
         relu<8>(A);
     }
-    if (save) {
-        store_native<8>(A, SV + nr_sv_h(0, nb) + (size_t)blk * NR_NATIVE(256), lane);
-        store_mask<8>(A, (uint32_t*)(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + 0) * 256,
-                      lane);
-    }
 
-#define NR_DENSE(DST, SRC, LOFF, L)                                                   \
-    init_bias<8>(DST, H + NR_H_BIAS(L), h);                                            \
-    mm_acc<128, 8>(P + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; });   \
-    relu<8>(DST);                                                                      \
-    if (save) {                                                                        \
-        store_native<8>(DST, SV + nr_sv_h(L - 1, nb) + (size_t)blk * NR_NATIVE(256), lane); \
-        store_mask<8>(DST, (uint32_t*)(SV + nr_sv_mask(nb)) +                          \
-                               ((size_t)blk * NR_MASK_LAYERS + L - 1) * 256, lane);    \
-    }
+#define NR_DENSE(DST, SRC, LOFF, L)                                                         \
+    init_bias<8>(DST, H + NR_H_BIAS(L), h);                                                  \
+    nr_mm_acc<128, 8>(P + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; },       \
+                      side_acc8(SRC, hseg(L - 2), mseg(L - 2)));                             \
+    relu<8>(DST);
 
-    NR_DENSE(B, A, NR_F_L2, 2)
+    NR_DENSE(B, A, NR_F_L2, 2)   // stores h1 while computing h2
     NR_DENSE(A, B, NR_F_L3, 3)
     NR_DENSE(B, A, NR_F_L4, 4)
     {   // layer 5: cat[PE, h4] -> 256 (skip, nerf.py:108-109); PE recomputed
@@ -212,15 +180,11 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         if constexpr (EMB) pe_gather<15, NR_PE_KSTEPS>(pe, xrow, h);
         else pe_encode<15, NR_PE_KSTEPS>(pe, px, py, pz, h);
         init_bias<8>(A, H + NR_H_BIAS(5), h);
-        mm_acc<NR_PE_KSTEPS, 8>(P + NR_F_L5, lane, A, [&](int g) { return pe[g]; });
-        mm_acc<128, 8>(P + NR_F_L5 + NR_PL(NR_PE_KSTEPS, 8), lane, A,
-                       [&](int g) { return B[g >> 4][g & 15]; });
+        nr_mm_acc<NR_PE_KSTEPS, 8>(P + NR_F_L5, lane, A, [&](int g) { return pe[g]; });
+        nr_mm_acc<128, 8>(P + NR_F_L5 + NR_PL(NR_PE_KSTEPS, 8), lane, A,
+                          [&](int g) { return B[g >> 4][g & 15]; },
+                          side_acc8(B, hseg(3), mseg(3)));
         relu<8>(A);
-        if (save) {
-            store_native<8>(A, SV + nr_sv_h(4, nb) + (size_t)blk * NR_NATIVE(256), lane);
-            store_mask<8>(A, (uint32_t*)(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + 4) * 256,
-                          lane);
-        }
     }
     NR_DENSE(B, A, NR_F_L6, 6)
     NR_DENSE(A, B, NR_F_L7, 7)
@@ -233,34 +197,30 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         if (valid && h == 0) a.out[s] = sigma;
         return;
     } else {
-        // xyz_encoding_final: Linear(256,256), no activation (nerf.py:116)
+        // xyz_encoding_final: Linear(256,256), no activation (nerf.py:116); stores h8
         init_bias<8>(A, H + NR_H_BFINAL, h);
-        mm_acc<128, 8>(P + NR_F_FINAL, lane, A, [&](int g) { return B[g >> 4][g & 15]; });
-        if (save) store_native<8>(A, SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256), lane);
+        nr_mm_acc<128, 8>(P + NR_F_FINAL, lane, A, [&](int g) { return B[g >> 4][g & 15]; },
+                          side_acc8(B, hseg(7), mseg(7)));
 
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
         float dpe[NR_DIR_KSTEPS];
         if constexpr (EMB) pe_gather<6, NR_DIR_KSTEPS>(dpe, xrow + NR_XYZ_CH, h);
         else pe_encode<6, NR_DIR_KSTEPS>(dpe, dx, dy, dz, h);
-        if (save) {
-            float* dst = SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32) + lane * 4;
-#pragma unroll
-            for (int gq = 0; gq < NR_DIR_KSTEPS / 4; ++gq) {
-                f32x4 v = {dpe[4 * gq], dpe[4 * gq + 1], dpe[4 * gq + 2], dpe[4 * gq + 3]};
-                *reinterpret_cast<f32x4*>(dst + gq * 256) = v;
-            }
-        }
         f32x16 C[4];
         init_bias<4>(C, H + NR_H_BDIR, h);
-        mm_acc<128, 4>(P + NR_F_DIR, lane, C, [&](int g) { return A[g >> 4][g & 15]; });
-        mm_acc<NR_DIR_KSTEPS, 4>(P + NR_F_DIR + NR_PL(128, 4), lane, C,
-                                 [&](int g) { return dpe[g]; });
+        float* fdst = SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256);
+        nr_mm_acc<128, 4>(P + NR_F_DIR, lane, C, [&](int g) { return A[g >> 4][g & 15]; },
+                          side_acc8(A, fdst, nullptr));
+        float* ddst = SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32);
+        nr_mm_acc<NR_DIR_KSTEPS, 4>(P + NR_F_DIR + NR_PL(128, 4), lane, C,
+                                    [&](int g) { return dpe[g]; },
+                                    [&](int grp) {
+                                        if (!save) return;
+                                        f32x4 v = {dpe[4 * grp], dpe[4 * grp + 1], dpe[4 * grp + 2],
+                                                   dpe[4 * grp + 3]};
+                                        *reinterpret_cast<f32x4*>(ddst + (grp * 64 + lane) * 4) = v;
+                                    });
         relu<4>(C);
-        if (save) {
-            store_native<4>(C, SV + nr_sv_hdir(nb) + (size_t)blk * NR_NATIVE(128), lane);
-            store_mask<4>(C, (uint32_t*)(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + 8) * 256,
-                          lane);
-        }
 
         // rgb = Sigmoid(Linear(128,3)) (nerf.py:79-81,120)
         float rgb[3];
@@ -272,6 +232,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         if (valid && h == 0) {
             f32x4 o = {rgb[0], rgb[1], rgb[2], sigma};
             *reinterpret_cast<f32x4*>(a.out + (size_t)s * 4) = o;
+        }
+        if (save) {   // hdir: last layer, stored at the end
+            store_native<4>(C, SV + nr_sv_hdir(nb) + (size_t)blk * NR_NATIVE(128), lane);
+            store_mask<4>(C, mseg(8), lane);
         }
     }
 }

@@ -72,31 +72,34 @@ struct WgArgs {
     float* slab;
 };
 
-// float4 count of one block of a segment
-__device__ __forceinline__ int seg_f4(const WgSeg& s) {
-    return s.kind == SEG_ACC ? s.width * 8 : (s.kind == SEG_HEAD ? 32 : s.width * 8);
-}
-// (sample j, first column) of float4 e of a block
-__device__ __forceinline__ void seg_pos(int kind, int e, int& j, int& c) {
-    j = e & 31;
-    switch (kind) {
-        case SEG_ACC: c = 32 * (e >> 8) + 8 * ((e >> 6) & 3) + 4 * ((e >> 5) & 1); break;
-        case SEG_PE:  c = 32 * ((e >> 5) & 1) + 4 * (e >> 6); break;
-        case SEG_DPE: c = 16 * ((e >> 5) & 1) + 4 * (e >> 6); break;
-        default:      c = 0; j = e; break;
+// Staging geometry of one 32-sample block of a segment, all compile time:
+// float4 e = tid + 256*i lands at LDS [sample j][column c].
+template <int KIND, int W>
+struct SegGeo {
+    static constexpr int F4 = KIND == SEG_HEAD ? 32 : W * 8;     // float4 per block
+    static constexpr int ITERS = (F4 + 255) / 256;
+    __device__ static __forceinline__ int j(int tid) { return KIND == SEG_HEAD ? tid : (tid & 31); }
+    // column of float4 #i of thread tid
+    __device__ static __forceinline__ int c(int tid, int i) {
+        const int h = (tid >> 5) & 1, w = tid >> 6;
+        if constexpr (KIND == SEG_ACC) return 32 * i + 8 * w + 4 * h;          // t = i, q = w
+        else if constexpr (KIND == SEG_PE) return 32 * h + 16 * i + 4 * w;     // gq = 4i + w
+        else if constexpr (KIND == SEG_DPE) return 16 * h + 4 * w;             // gq = w
+        else return 0;
     }
-}
+};
 
-template <int MT, int NT>
+template <int KA, int WA, int KB, int WB, int WM, int WN>
 __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int b0, int b1,
                                            float* lds, float* __restrict__ slab) {
+    using GA = SegGeo<KA, WA>;
+    using GB = SegGeo<KB, WB>;
+    constexpr int MT = (WA / WM + 31) / 32, NT = (WB / WN + 31) / 32;
+    constexpr int M = WA, N = WB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int mi = wave / T.wn, ni = wave % T.wn;
+    const int mi = wave / WN, ni = wave % WN;
     const int m0 = 32 * MT * mi, n0 = 32 * NT * ni;
-    const int M = T.a.width, N = T.b.width;
     const bool do_bias = ni == 0;
-    const int fa = seg_f4(T.a), fb = seg_f4(T.b);
-    const int blk_a = T.a.width * 32, blk_b = T.b.width * 32;   // floats per block
 
     f32x16 acc[MT][NT];
 #pragma unroll
@@ -107,31 +110,36 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
 #pragma unroll
     for (int i = 0; i < MT; ++i) bsum[i] = 0.f;
 
-    f32x4 ra[8], rb[8];
+    // per-thread staging addresses: global float4 index tid + 256 i, LDS [j][c]
+    const bool ta = tid < GA::F4, tb = tid < GB::F4;
+    const int ja = GA::j(tid), jb = GB::j(tid);
+    f32x4 ra[GA::ITERS], rb[GB::ITERS];
     auto load = [&](int blk) {
-        const int nval = a.n - blk * 32;            // valid samples in this block
-        const f32x4* pa = reinterpret_cast<const f32x4*>(T.a.base + (size_t)blk * blk_a);
-        const f32x4* pb = reinterpret_cast<const f32x4*>(T.b.base + (size_t)blk * blk_b);
+        const f32x4* pa = reinterpret_cast<const f32x4*>(T.a.base) + (size_t)blk * GA::F4 + tid;
+        const f32x4* pb = reinterpret_cast<const f32x4*>(T.b.base) + (size_t)blk * GB::F4 + tid;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int e = tid + 256 * i;
-            int j, c;
-            ra[i] = f32x4{};
-            rb[i] = f32x4{};
-            if (e < fa) { seg_pos(T.a.kind, e, j, c); if (j < nval) ra[i] = pa[e]; }
-            if (e < fb) { seg_pos(T.b.kind, e, j, c); if (j < nval) rb[i] = pb[e]; }
+        for (int i = 0; i < GA::ITERS; ++i) ra[i] = ta ? pa[256 * i] : f32x4{};
+#pragma unroll
+        for (int i = 0; i < GB::ITERS; ++i) rb[i] = tb ? pb[256 * i] : f32x4{};
+        const int nval = a.n - blk * 32;
+        if (nval < 32) {          // tail block (uniform branch): zero samples >= n
+#pragma unroll
+            for (int i = 0; i < GA::ITERS; ++i) if (ja >= nval) ra[i] = f32x4{};
+#pragma unroll
+            for (int i = 0; i < GB::ITERS; ++i) if (jb >= nval) rb[i] = f32x4{};
         }
     };
     auto store = [&](int buf) {
-        float* la = lds + buf * (2 * 32 * kRow);
-        float* lb = la + 32 * kRow;
+        float* la = lds + buf * (2 * 32 * kRow) + ja * kRow;
+        float* lb = lds + buf * (2 * 32 * kRow) + 32 * kRow + jb * kRow;
+        if (ta)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int e = tid + 256 * i;
-            int j, c;
-            if (e < fa) { seg_pos(T.a.kind, e, j, c); *reinterpret_cast<f32x4*>(la + j * kRow + c) = ra[i]; }
-            if (e < fb) { seg_pos(T.b.kind, e, j, c); *reinterpret_cast<f32x4*>(lb + j * kRow + c) = rb[i]; }
-        }
+            for (int i = 0; i < GA::ITERS; ++i)
+                *reinterpret_cast<f32x4*>(la + GA::c(tid, i)) = ra[i];
+        if (tb)
+#pragma unroll
+            for (int i = 0; i < GB::ITERS; ++i)
+                *reinterpret_cast<f32x4*>(lb + GB::c(tid, i)) = rb[i];
     };
 
     const int nst = b1 - b0;
@@ -145,17 +153,15 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
     for (int st = 0; st < nst; ++st) {
         const int buf = st & 1;
         if (st + 1 < nst) load(b0 + st + 1);
-        const float* la = lds + buf * (2 * 32 * kRow);
-        const float* lb = la + 32 * kRow;
+        const float* la = lds + buf * (2 * 32 * kRow) + h * kRow + m0 + col;
+        const float* lb = lds + buf * (2 * 32 * kRow) + 32 * kRow + h * kRow + n0 + col;
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) {
-            const float* ar = la + (2 * kk + h) * kRow + m0 + col;
-            const float* br = lb + (2 * kk + h) * kRow + n0 + col;
             float av[MT], bv[NT];
 #pragma unroll
-            for (int i = 0; i < MT; ++i) av[i] = ar[32 * i];
+            for (int i = 0; i < MT; ++i) av[i] = la[2 * kk * kRow + 32 * i];
 #pragma unroll
-            for (int j = 0; j < NT; ++j) bv[j] = br[32 * j];
+            for (int j = 0; j < NT; ++j) bv[j] = lb[2 * kk * kRow + 32 * j];
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -195,14 +201,20 @@ __global__ void __launch_bounds__(256, 1) wgrad_kernel(WgArgs a) {
     const int b0 = (int)((int64_t)c * a.nb / T.G);
     const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
     float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
-    const int M = T.a.width, N = T.b.width;
-    const int key = __builtin_amdgcn_readfirstlane(((M / T.wm + 31) / 32) * 8 + (N / T.wn + 31) / 32);
-    switch (key) {
-        case 4 * 8 + 4: wgrad_body<4, 4>(a, T, b0, b1, lds, slab); break;
-        case 2 * 8 + 4: wgrad_body<2, 4>(a, T, b0, b1, lds, slab); break;
-        case 2 * 8 + 2: wgrad_body<2, 2>(a, T, b0, b1, lds, slab); break;
-        case 1 * 8 + 2: wgrad_body<1, 2>(a, T, b0, b1, lds, slab); break;
-        default:        wgrad_body<1, 1>(a, T, b0, b1, lds, slab); break;
+    // task shapes (see nr_wgrad's task list); wave-uniform
+    switch (__builtin_amdgcn_readfirstlane(t)) {
+        case 0: case 4:
+            wgrad_body<SEG_ACC, 256, SEG_PE, 64, 4, 1>(a, T, b0, b1, lds, slab); break;
+        case 10:
+            wgrad_body<SEG_ACC, 128, SEG_ACC, 256, 2, 2>(a, T, b0, b1, lds, slab); break;
+        case 11:
+            wgrad_body<SEG_ACC, 128, SEG_DPE, 32, 4, 1>(a, T, b0, b1, lds, slab); break;
+        case 12:
+            wgrad_body<SEG_HEAD, 4, SEG_ACC, 256, 1, 4>(a, T, b0, b1, lds, slab); break;
+        case 13:
+            wgrad_body<SEG_HEAD, 4, SEG_ACC, 128, 1, 4>(a, T, b0, b1, lds, slab); break;
+        default:
+            wgrad_body<SEG_ACC, 256, SEG_ACC, 256, 2, 2>(a, T, b0, b1, lds, slab); break;
     }
 }
 
