@@ -135,6 +135,7 @@ __device__ __forceinline__ void nr_mm_acc(const float* __restrict__ w, int lane,
     for (int grp = 0; grp < KS / 4; grp += 2) {
         nr_ld_wgrp<NT>(w, grp + 1, lane, wb);
         side(grp);
+        __builtin_amdgcn_sched_barrier(0);   // keep the prefetch a full group ahead
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const float b = getb(grp * 4 + kk);
@@ -143,6 +144,7 @@ __device__ __forceinline__ void nr_mm_acc(const float* __restrict__ w, int lane,
         }
         if (grp + 2 < KS / 4) nr_ld_wgrp<NT>(w, grp + 2, lane, wa);
         side(grp + 1);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const float b = getb(grp * 4 + 4 + kk);

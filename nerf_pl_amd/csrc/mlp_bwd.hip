@@ -52,11 +52,24 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     const float* H = a.packed_fwd + NR_F_HEAD;
     const float* SV = a.save;
     float* const GD = a.grad;
-    const uint4* mask = reinterpret_cast<const uint4*>(SV + nr_sv_mask(nb)) +
-                        (size_t)blk * NR_MASK_LAYERS * 64 + lane;   // [layer][lane]
+    // The wave's 9 ReLU-mask words per lane arrive by LDS-DMA up front (one
+    // HBM round trip per wave); per-layer HBM loads would otherwise sit in
+    // front of every weight-load wait (vmcnt retires in issue order).
+    __shared__ __attribute__((aligned(16))) uint4 smask[kWaves][NR_MASK_LAYERS][64];
+    {
+        const uint4* gm = reinterpret_cast<const uint4*>(SV + nr_sv_mask(nb)) +
+                          (size_t)blk * NR_MASK_LAYERS * 64 + lane;
+#pragma unroll
+        for (int l = 0; l < NR_MASK_LAYERS; ++l)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(gm + l * 64),
+                (__attribute__((address_space(3))) void*)&smask[wave][l][0], 16, 0, 0);
+    }
+    const uint4* mask = &smask[wave][0][lane];   // [layer * 64]
 
     const f32x4 go = *reinterpret_cast<const f32x4*>(a.g_out + (size_t)s * 4);
     const f32x4 yo = *reinterpret_cast<const f32x4*>(a.out + (size_t)s * 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // masks landed in LDS (own wave only)
     // sigmoid backward: grad * (1 - y) * y  (ATen sigmoid_backward); tail lanes -> 0
     float dzr[3];
 #pragma unroll
