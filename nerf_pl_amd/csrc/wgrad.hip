@@ -18,7 +18,7 @@
 namespace {
 
 constexpr int kTasks = 14;
-constexpr int kTargetWG = 480;   // ~2 rounds of one workgroup per CU
+constexpr int kTargetWG = 760;   // ~3 rounds of one workgroup per CU (short tail)
 constexpr int kRow = 260;        // LDS row stride (floats)
 
 enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
@@ -118,34 +118,30 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
         const f32x4* pa = reinterpret_cast<const f32x4*>(T.a.base) + (size_t)blk * GA::F4 + tid;
         const f32x4* pb = reinterpret_cast<const f32x4*>(T.b.base) + (size_t)blk * GB::F4 + tid;
 #pragma unroll
-        for (int i = 0; i < GA::ITERS; ++i) ra[i] = ta ? pa[256 * i] : f32x4{};
+        for (int i = 0; i < GA::ITERS; ++i) if (ta) ra[i] = pa[256 * i];
 #pragma unroll
-        for (int i = 0; i < GB::ITERS; ++i) rb[i] = tb ? pb[256 * i] : f32x4{};
-        const int nval = a.n - blk * 32;
-        if (nval < 32) {          // tail block (uniform branch): zero samples >= n
-#pragma unroll
-            for (int i = 0; i < GA::ITERS; ++i) if (ja >= nval) ra[i] = f32x4{};
-#pragma unroll
-            for (int i = 0; i < GB::ITERS; ++i) if (jb >= nval) rb[i] = f32x4{};
-        }
+        for (int i = 0; i < GB::ITERS; ++i) if (tb) rb[i] = pb[256 * i];
     };
-    auto store = [&](int buf) {
+    // write the staged block to LDS; samples >= n of the tail block become 0
+    auto store = [&](int buf, int blk) {
+        const int nval = a.n - blk * 32;
+        const bool ka = ja < nval, kb = jb < nval;
         float* la = lds + buf * (2 * 32 * kRow) + ja * kRow;
         float* lb = lds + buf * (2 * 32 * kRow) + 32 * kRow + jb * kRow;
         if (ta)
 #pragma unroll
             for (int i = 0; i < GA::ITERS; ++i)
-                *reinterpret_cast<f32x4*>(la + GA::c(tid, i)) = ra[i];
+                *reinterpret_cast<f32x4*>(la + GA::c(tid, i)) = ka ? ra[i] : f32x4{};
         if (tb)
 #pragma unroll
             for (int i = 0; i < GB::ITERS; ++i)
-                *reinterpret_cast<f32x4*>(lb + GB::c(tid, i)) = rb[i];
+                *reinterpret_cast<f32x4*>(lb + GB::c(tid, i)) = kb ? rb[i] : f32x4{};
     };
 
     const int nst = b1 - b0;
     if (nst > 0) {
         load(b0);
-        store(0);
+        store(0, b0);
     }
     __syncthreads();
     const int h = lane >> 5, col = lane & 31;
@@ -155,22 +151,34 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
         if (st + 1 < nst) load(b0 + st + 1);
         const float* la = lds + buf * (2 * 32 * kRow) + h * kRow + m0 + col;
         const float* lb = lds + buf * (2 * 32 * kRow) + 32 * kRow + h * kRow + n0 + col;
+        // operands double-buffered one k-step ahead (LDS latency off the MFMA path)
+        float av[2][MT], bv[2][NT];
+        auto rd = [&](int kk, int p) {
 #pragma unroll
-        for (int kk = 0; kk < 16; ++kk) {
-            float av[MT], bv[NT];
+            for (int i = 0; i < MT; ++i) av[p][i] = la[2 * kk * kRow + 32 * i];
 #pragma unroll
-            for (int i = 0; i < MT; ++i) av[i] = la[2 * kk * kRow + 32 * i];
-#pragma unroll
-            for (int j = 0; j < NT; ++j) bv[j] = lb[2 * kk * kRow + 32 * j];
+            for (int j = 0; j < NT; ++j) bv[p][j] = lb[2 * kk * kRow + 32 * j];
+        };
+        auto mm = [&](int p) {
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
-                for (int j = 0; j < NT; ++j) acc[i][j] = nr_mfma32(av[i], bv[j], acc[i][j]);
+                for (int j = 0; j < NT; ++j) acc[i][j] = nr_mfma32(av[p][i], bv[p][j], acc[i][j]);
             if (do_bias)
 #pragma unroll
-                for (int i = 0; i < MT; ++i) bsum[i] += av[i];
+                for (int i = 0; i < MT; ++i) bsum[i] += av[p][i];
+        };
+        rd(0, 0);
+#pragma unroll
+        for (int kk = 0; kk < 16; kk += 2) {
+            rd(kk + 1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mm(0);
+            if (kk + 2 < 16) rd(kk + 2, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            mm(1);
         }
-        if (st + 1 < nst) store(buf ^ 1);
+        if (st + 1 < nst) store(buf ^ 1, b0 + st + 1);
         __syncthreads();
     }
 #pragma unroll
@@ -302,12 +310,17 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
         {head, H(7), 1, 4}, {head, hdir, 1, 4},
     };
     WgArgs a{};
-    int cost[kTasks], tot = 0;
+    // per-block cost of a task's workgroup, in cycles: its waves' MFMA time,
+    // or the staging of (M + N) x 32 floats at ~8 B/cycle per CU, plus a
+    // fixed barrier/LDS-store overhead
+    int64_t cost[kTasks], tot = 0;
     for (int t = 0; t < kTasks; ++t) {
         a.task[t] = tasks[t];
         const int mt = (tasks[t].a.width / tasks[t].wm + 31) / 32;
         const int nt = (tasks[t].b.width / tasks[t].wn + 31) / 32;
-        cost[t] = mt * nt;   // MFMAs per k-step of each (equally loaded) wave
+        const int64_t mfma = 16 * mt * nt * 64;
+        const int64_t bytes = (int64_t)(tasks[t].a.width + tasks[t].b.width) * 32 * 4;
+        cost[t] = std::max<int64_t>(mfma, bytes / 8) + 512;
         tot += cost[t];
     }
     a.wg_start[0] = 0;
