@@ -1,0 +1,67 @@
+"""Multi-process (world_size 2, gloo, CPU) check of the data-parallel exchange:
+after GradAllReducer every rank holds the mean gradient, identical to what a
+single process computes on the union of the ranks' batches (the property
+SURVEY.md 4 asks for: k ranks reproduce the 1-rank averaged gradient)."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nerf_pl_amd.distributed import GradAllReducer
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ReLU(), torch.nn.Linear(7, 3))
+        unused = torch.nn.Parameter(torch.ones(2))           # never gets a gradient
+        g = torch.Generator().manual_seed(100)
+        x_all = torch.randn(8, 5, generator=g)
+        y_all = torch.randn(8, 3, generator=g)
+        x, y = x_all[rank::world], y_all[rank::world]
+        loss = ((model(x) - y) ** 2).mean()
+        loss.backward()
+        red = GradAllReducer(list(model.parameters()) + [unused])
+        red()
+        q.put((rank, [p.grad.clone() for p in model.parameters()], unused.grad.clone()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_matches_single_process():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference: mean of per-rank mean-losses == average of grads
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ReLU(), torch.nn.Linear(7, 3))
+    g = torch.Generator().manual_seed(100)
+    x_all = torch.randn(8, 5, generator=g)
+    y_all = torch.randn(8, 3, generator=g)
+    loss = sum(((model(x_all[r::world]) - y_all[r::world]) ** 2).mean() for r in range(world)) / world
+    loss.backward()
+    ref = [p.grad for p in model.parameters()]
+    for rank, grads, ug in res:
+        for a, b in zip(grads, ref):
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+        assert torch.all(ug == 0)
