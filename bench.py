@@ -62,22 +62,6 @@ class KernelTimer:
         self.events = {}
         self.enabled = False
 
-    def wrap(self, mod, fname, tag_fn):
-        orig = getattr(mod, fname)
-
-        def wrapped(*a, **k):
-            if not self.enabled:
-                return orig(*a, **k)
-            tag, n = tag_fn(*a, **k)
-            s = torch.cuda.Event(enable_timing=True)
-            e = torch.cuda.Event(enable_timing=True)
-            s.record()
-            r = orig(*a, **k)
-            e.record()
-            self.events.setdefault(tag, []).append((s, e, n))
-            return r
-        setattr(mod, fname, wrapped)
-
     def summary(self):
         out = {}
         for tag, lst in self.events.items():
@@ -231,8 +215,16 @@ def main():
         durs = [t for t, n in big if n == nmax]
         avg = sum(durs) / len(durs)
         ach = flop[dom] * nmax / (avg * 1e-3) / 1e12
+        traffic, tsrc = None, None
+        tf = os.path.join(REPO, "profiles", "r01", "traffic.json")
+        if os.path.exists(tf):
+            t = json.load(open(tf)).get(dom)
+            if t and int(t["samples"]) == nmax:
+                traffic = round(t["hbm_bytes"] / 1e9, 3)
+                tsrc = f"profiles/r01/traffic.json ({t['method']})"
         roof = dict(bound="mfma", kernel=dom, achieved=round(ach, 2), peak=FP32_MFMA_PEAK_TF,
-                    unit="TFLOP/s", frac=round(ach / FP32_MFMA_PEAK_TF, 4), traffic=None,
+                    unit="TFLOP/s", frac=round(ach / FP32_MFMA_PEAK_TF, 4), traffic=traffic,
+                    traffic_unit="GB per launch", traffic_source=tsrc,
                     samples_per_launch=nmax, avg_launch_ms=round(avg, 4),
                     flop_per_sample=flop[dom])
         d["share_of_step"] = d["total_ms"] / (ms * args.steps)
