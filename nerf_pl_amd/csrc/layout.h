@@ -121,16 +121,30 @@ __device__ __forceinline__ void nr_ld_wgrp(const float* __restrict__ w, int grp,
     for (int t = 0; t < NT; ++t) dst[t] = p[t * 64];
 }
 
+// load group grp of a packed layer (N tiles) into the first N slots of dst
+template <int N>
+__device__ __forceinline__ void nr_ld_into(const float* __restrict__ w, int grp, int lane,
+                                           f32x4 (&dst)[8]) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(w) + (size_t)grp * N * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < N; ++t) dst[t] = p[t * 64];
+}
+
 struct NrNoSide {
     __device__ __forceinline__ void operator()(int) const {}
 };
 
-template <int KS, int NT, typename GetB, typename Side = NrNoSide>
-__device__ __forceinline__ void nr_mm_acc(const float* __restrict__ w, int lane, f32x16 (&acc)[NT],
-                                          GetB getb, Side side = Side()) {
+// Chained form: on entry wa[0..NT) already holds (or is loading) group 0 of
+// w; when w_next != nullptr the first group of the next layer (NTN tiles) is
+// prefetched into wa as soon as wa is free, so no layer starts with a cold
+// L2/MALL round trip.
+template <int KS, int NT, int NTN, typename GetB, typename Side = NrNoSide>
+__device__ __forceinline__ void nr_mm_chain(const float* __restrict__ w,
+                                            const float* __restrict__ w_next, int lane,
+                                            f32x16 (&acc)[NT], f32x4 (&wa)[8], GetB getb,
+                                            Side side = Side()) {
     static_assert(KS % 8 == 0, "k-steps must be a multiple of 8");
-    f32x4 wa[NT], wb[NT];
-    nr_ld_wgrp<NT>(w, 0, lane, wa);
+    f32x4 wb[NT];
 #pragma unroll
     for (int grp = 0; grp < KS / 4; grp += 2) {
         nr_ld_wgrp<NT>(w, grp + 1, lane, wb);
@@ -142,7 +156,8 @@ __device__ __forceinline__ void nr_mm_acc(const float* __restrict__ w, int lane,
 #pragma unroll
             for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wa[t][kk], b, acc[t]);
         }
-        if (grp + 2 < KS / 4) nr_ld_wgrp<NT>(w, grp + 2, lane, wa);
+        if (grp + 2 < KS / 4) nr_ld_into<NT>(w, grp + 2, lane, wa);
+        else if (w_next != nullptr) nr_ld_into<NTN>(w_next, 0, lane, wa);
         side(grp + 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -152,6 +167,11 @@ __device__ __forceinline__ void nr_mm_acc(const float* __restrict__ w, int lane,
             for (int t = 0; t < NT; ++t) acc[t] = nr_mfma32(wb[t][kk], b, acc[t]);
         }
     }
+}
+
+template <int NT>
+__device__ __forceinline__ void nr_ld_first(const float* __restrict__ w, int lane, f32x4 (&wa)[8]) {
+    nr_ld_into<NT>(w, 0, lane, wa);
 }
 
 // piece p (= 4t + q) of a block-native store: one float4 per lane

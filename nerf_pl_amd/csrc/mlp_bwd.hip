@@ -67,6 +67,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     }
     const uint4* mask = &smask[wave][0][lane];   // [layer * 64]
 
+    f32x4 wq[8];                 // weight group in flight across layer boundaries
+    nr_ld_first<8>(PB + NR_B_DIRT, lane, wq);
     const f32x4 go = *reinterpret_cast<const f32x4*>(a.g_out + (size_t)s * 4);
     const f32x4 yo = *reinterpret_cast<const f32x4*>(a.out + (size_t)s * 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // masks landed in LDS (own wave only)
@@ -111,8 +113,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     zero<8>(A);
     {
         float* cdst = GD + nr_gd_dzdir(nb) + (size_t)blk * NR_NATIVE(128);
-        nr_mm_acc<64, 8>(PB + NR_B_DIRT, lane, A, [&](int g) { return C[g >> 4][g & 15]; },
-                         [&](int grp) { store_native_piece<4>(C, grp, cdst, lane); });
+        nr_mm_chain<64, 8, 8>(PB + NR_B_DIRT, PB + NR_B_FINALT, lane, A, wq,
+                              [&](int g) { return C[g >> 4][g & 15]; },
+                              [&](int grp) { store_native_piece<4>(C, grp, cdst, lane); });
     }
 
     // d h8 = W_final^T dfeat + W_sigma^T dsigma, masked by h8; stores dfeat
@@ -126,27 +129,28 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
         }
     {
         const uint4 mk = mask[7 * 64];
-        nr_mm_acc<128, 8>(PB + NR_B_FINALT, lane, B, [&](int g) { return A[g >> 4][g & 15]; },
-                          side8(A, dzseg(8)));
+        nr_mm_chain<128, 8, 8>(PB + NR_B_FINALT, PB + NR_B_L8T, lane, B, wq,
+                               [&](int g) { return A[g >> 4][g & 15]; }, side8(A, dzseg(8)));
         relu_mask<8>(B, mk);
     }
 
-#define NR_BACK(DST, SRC, LOFF, L)                                                           \
+#define NR_BACK(DST, SRC, LOFF, NEXT, L)                                                     \
     {                                                                                         \
         const uint4 mk = mask[(L - 1) * 64];                                                  \
         zero<8>(DST);                                                                         \
-        nr_mm_acc<128, 8>(PB + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; },   \
-                          side8(SRC, dzseg(L)));                                              \
+        nr_mm_chain<128, 8, 8>(PB + LOFF, NEXT, lane, DST, wq,                                \
+                               [&](int g) { return SRC[g >> 4][g & 15]; },                    \
+                               side8(SRC, dzseg(L)));                                         \
         relu_mask<8>(DST, mk);                                                                \
     }
 
-    NR_BACK(A, B, NR_B_L8T, 7)   // dz7 = (W8^T dz8) * [h7 > 0], stores dz8
-    NR_BACK(B, A, NR_B_L7T, 6)
-    NR_BACK(A, B, NR_B_L6T, 5)
-    NR_BACK(B, A, NR_B_L5T, 4)   // through the h4 columns of the skip layer
-    NR_BACK(A, B, NR_B_L4T, 3)
-    NR_BACK(B, A, NR_B_L3T, 2)
-    NR_BACK(A, B, NR_B_L2T, 1)   // stores dz2, leaves dz1 in A
+    NR_BACK(A, B, NR_B_L8T, PB + NR_B_L7T, 7)   // dz7 = (W8^T dz8) * [h7 > 0], stores dz8
+    NR_BACK(B, A, NR_B_L7T, PB + NR_B_L6T, 6)
+    NR_BACK(A, B, NR_B_L6T, PB + NR_B_L5T, 5)
+    NR_BACK(B, A, NR_B_L5T, PB + NR_B_L4T, 4)   // through the h4 columns of the skip layer
+    NR_BACK(A, B, NR_B_L4T, PB + NR_B_L3T, 3)
+    NR_BACK(B, A, NR_B_L3T, PB + NR_B_L2T, 2)
+    NR_BACK(A, B, NR_B_L2T, nullptr, 1)         // stores dz2, leaves dz1 in A
 #undef NR_BACK
     store_native<8>(A, dzseg(0), lane);
 }

@@ -114,7 +114,16 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     const bool valid = s_raw < a.n;
     const int s = valid ? s_raw : a.n - 1;
     const float* P = a.packed;
-    const float* H = a.packed + NR_F_HEAD;
+    // biases and the sigma/rgb heads come from LDS so their reads never queue
+    // behind in-flight weight loads (vmcnt retires in issue order)
+    __shared__ __attribute__((aligned(16))) float Hs[NR_H_SIZE];
+    {
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.packed + NR_F_HEAD);
+        for (int i = threadIdx.x; i < NR_H_SIZE / 4; i += 64 * kWaves)
+            reinterpret_cast<f32x4*>(Hs)[i] = src[i];
+        __syncthreads();
+    }
+    const float* H = Hs;
     const int nb = (a.n + 31) / 32;
     const bool save = a.save != nullptr && blk < nb;     // whole block, tail lanes included
     float* const SV = a.save;
@@ -137,8 +146,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     }
 
     f32x16 A[8], B[8];
+    f32x4 wq[8];                 // weight group in flight across layer boundaries
+    nr_ld_first<8>(P + NR_F_L1, lane, wq);
     // Saved-activation stores (training): each layer's output is written while
-    // the next layer runs (nr_mm_acc side hook), one float4 per weight group.
+    // the next layer runs (side hook), one float4 per weight group.
     auto hseg = [&](int l) { return SV + nr_sv_h(l, nb) + (size_t)blk * NR_NATIVE(256); };
     auto mseg = [&](int l) {
         return reinterpret_cast<uint32_t*>(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + l) * 256;
@@ -156,39 +167,48 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         else pe_encode<15, NR_PE_KSTEPS>(pe, px, py, pz, h);
         float* pdst = SV + (size_t)blk * NR_NATIVE(64);
         init_bias<8>(A, H + NR_H_BIAS(1), h);
-        nr_mm_acc<NR_PE_KSTEPS, 8>(P + NR_F_L1, lane, A, [&](int g) { return pe[g]; },
-                                   [&](int grp) {
-                                       if (!save) return;
-                                       f32x4 v = {pe[4 * grp], pe[4 * grp + 1], pe[4 * grp + 2],
-                                                  pe[4 * grp + 3]};
-                                       *reinterpret_cast<f32x4*>(pdst + (grp * 64 + lane) * 4) = v;
-                                   });
+        nr_mm_chain<NR_PE_KSTEPS, 8, 8>(P + NR_F_L1, P + NR_F_L2, lane, A, wq,
+                                        [&](int g) { return pe[g]; },
+                                        [&](int grp) {
+                                            if (!save) return;
+                                            f32x4 v = {pe[4 * grp], pe[4 * grp + 1], pe[4 * grp + 2],
+                                                       pe[4 * grp + 3]};
+                                            *reinterpret_cast<f32x4*>(pdst + (grp * 64 + lane) * 4) = v;
+                                        });
         relu<8>(A);
     }
 
-#define NR_DENSE(DST, SRC, LOFF, L)                                                         \
-    init_bias<8>(DST, H + NR_H_BIAS(L), h);                                                  \
-    nr_mm_acc<128, 8>(P + LOFF, lane, DST, [&](int g) { return SRC[g >> 4][g & 15]; },       \
-                      side_acc8(SRC, hseg(L - 2), mseg(L - 2)));                             \
+#define NR_DENSE(DST, SRC, LOFF, NEXT, L)                                                    \
+    init_bias<8>(DST, H + NR_H_BIAS(L), h);                                                   \
+    nr_mm_chain<128, 8, 8>(P + LOFF, P + NEXT, lane, DST, wq,                                 \
+                           [&](int g) { return SRC[g >> 4][g & 15]; },                        \
+                           side_acc8(SRC, hseg(L - 2), mseg(L - 2)));                         \
     relu<8>(DST);
 
-    NR_DENSE(B, A, NR_F_L2, 2)   // stores h1 while computing h2
-    NR_DENSE(A, B, NR_F_L3, 3)
-    NR_DENSE(B, A, NR_F_L4, 4)
+    NR_DENSE(B, A, NR_F_L2, NR_F_L3, 2)   // stores h1 while computing h2
+    NR_DENSE(A, B, NR_F_L3, NR_F_L4, 3)
+    NR_DENSE(B, A, NR_F_L4, NR_F_L5, 4)
     {   // layer 5: cat[PE, h4] -> 256 (skip, nerf.py:108-109); PE recomputed
         float pe[NR_PE_KSTEPS];
         if constexpr (EMB) pe_gather<15, NR_PE_KSTEPS>(pe, xrow, h);
         else pe_encode<15, NR_PE_KSTEPS>(pe, px, py, pz, h);
         init_bias<8>(A, H + NR_H_BIAS(5), h);
-        nr_mm_acc<NR_PE_KSTEPS, 8>(P + NR_F_L5, lane, A, [&](int g) { return pe[g]; });
-        nr_mm_acc<128, 8>(P + NR_F_L5 + NR_PL(NR_PE_KSTEPS, 8), lane, A,
-                          [&](int g) { return B[g >> 4][g & 15]; },
-                          side_acc8(B, hseg(3), mseg(3)));
+        const float* l5h = P + NR_F_L5 + NR_PL(NR_PE_KSTEPS, 8);
+        nr_mm_chain<NR_PE_KSTEPS, 8, 8>(P + NR_F_L5, l5h, lane, A, wq, [&](int g) { return pe[g]; });
+        nr_mm_chain<128, 8, 8>(l5h, P + NR_F_L6, lane, A, wq,
+                               [&](int g) { return B[g >> 4][g & 15]; },
+                               side_acc8(B, hseg(3), mseg(3)));
         relu<8>(A);
     }
-    NR_DENSE(B, A, NR_F_L6, 6)
-    NR_DENSE(A, B, NR_F_L7, 7)
-    NR_DENSE(B, A, NR_F_L8, 8)
+    NR_DENSE(B, A, NR_F_L6, NR_F_L7, 6)
+    NR_DENSE(A, B, NR_F_L7, NR_F_L8, 7)
+    {   // layer 8 (chains into `final` unless sigma-only)
+        init_bias<8>(B, H + NR_H_BIAS(8), h);
+        nr_mm_chain<128, 8, 8>(P + NR_F_L8, SIGMA_ONLY ? nullptr : P + NR_F_FINAL, lane, B, wq,
+                               [&](int g) { return A[g >> 4][g & 15]; },
+                               side_acc8(A, hseg(6), mseg(6)));
+        relu<8>(B);
+    }
 #undef NR_DENSE
 
     // sigma = Linear(256, 1)(h8), raw (nerf.py:112)
@@ -199,8 +219,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     } else {
         // xyz_encoding_final: Linear(256,256), no activation (nerf.py:116); stores h8
         init_bias<8>(A, H + NR_H_BFINAL, h);
-        nr_mm_acc<128, 8>(P + NR_F_FINAL, lane, A, [&](int g) { return B[g >> 4][g & 15]; },
-                          side_acc8(B, hseg(7), mseg(7)));
+        nr_mm_chain<128, 8, 4>(P + NR_F_FINAL, P + NR_F_DIR, lane, A, wq,
+                               [&](int g) { return B[g >> 4][g & 15]; },
+                               side_acc8(B, hseg(7), mseg(7)));
 
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
         float dpe[NR_DIR_KSTEPS];
@@ -209,17 +230,19 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         f32x16 C[4];
         init_bias<4>(C, H + NR_H_BDIR, h);
         float* fdst = SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256);
-        nr_mm_acc<128, 4>(P + NR_F_DIR, lane, C, [&](int g) { return A[g >> 4][g & 15]; },
-                          side_acc8(A, fdst, nullptr));
+        const float* dpw = P + NR_F_DIR + NR_PL(128, 4);
+        nr_mm_chain<128, 4, 4>(P + NR_F_DIR, dpw, lane, C, wq,
+                               [&](int g) { return A[g >> 4][g & 15]; },
+                               side_acc8(A, fdst, nullptr));
         float* ddst = SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32);
-        nr_mm_acc<NR_DIR_KSTEPS, 4>(P + NR_F_DIR + NR_PL(128, 4), lane, C,
-                                    [&](int g) { return dpe[g]; },
-                                    [&](int grp) {
-                                        if (!save) return;
-                                        f32x4 v = {dpe[4 * grp], dpe[4 * grp + 1], dpe[4 * grp + 2],
-                                                   dpe[4 * grp + 3]};
-                                        *reinterpret_cast<f32x4*>(ddst + (grp * 64 + lane) * 4) = v;
-                                    });
+        nr_mm_chain<NR_DIR_KSTEPS, 4, 4>(dpw, nullptr, lane, C, wq,
+                                         [&](int g) { return dpe[g]; },
+                                         [&](int grp) {
+                                             if (!save) return;
+                                             f32x4 v = {dpe[4 * grp], dpe[4 * grp + 1],
+                                                        dpe[4 * grp + 2], dpe[4 * grp + 3]};
+                                             *reinterpret_cast<f32x4*>(ddst + (grp * 64 + lane) * 4) = v;
+                                         });
         relu<4>(C);
 
         // rgb = Sigmoid(Linear(128,3)) (nerf.py:79-81,120)
