@@ -13,6 +13,8 @@
 // Each workgroup writes one partial slab; a second kernel sums a task's slabs
 // in a fixed order (bitwise reproducible) and scatters the result into the flat
 // gradient buffer in NeRF.named_parameters() order.
+#include <stdlib.h>
+
 #include "layout.h"
 
 namespace {
@@ -325,9 +327,14 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
     }
     a.wg_start[0] = 0;
     int64_t slab = 0;
+    // diagnostic: NR_WGRAD_TASKMASK limits the launch to a subset of tasks (the
+    // kernel code is unchanged; gradients of the other tasks are then stale)
+    static const long long tmask =
+        getenv("NR_WGRAD_TASKMASK") ? strtoll(getenv("NR_WGRAD_TASKMASK"), nullptr, 0) : -1;
     for (int t = 0; t < kTasks; ++t) {
         int64_t g = (kTargetWG * cost[t] + tot - 1) / tot;   // per-workgroup work <= target
         g = std::max<int64_t>(1, std::min<int64_t>(g, nb));
+        if (!((tmask >> t) & 1)) g = 0;
         a.task[t].G = (int)g;
         a.task[t].slab = slab;
         slab += (int64_t)g * (tasks[t].a.width * tasks[t].b.width + tasks[t].a.width);
