@@ -21,6 +21,8 @@ namespace {
 
 constexpr int kTasks = 14;
 constexpr int kTargetWG = 760;   // ~3 rounds of one workgroup per CU (short tail)
+constexpr int kThreads = 512;    // 8 waves: two per SIMD, so one wave's staging and
+                                 // barrier time overlaps its partner's MFMAs
 constexpr int kRow = 260;        // LDS row stride (floats)
 
 enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
@@ -75,18 +77,19 @@ struct WgArgs {
 };
 
 // Staging geometry of one 32-sample block of a segment, all compile time:
-// float4 e = tid + 256*i lands at LDS [sample j][column c].
+// float4 e = tid + 512*i lands at LDS [sample j][column c].  In the
+// block-native order float4 e is (t = e>>8, q = (e>>6)&3, lane = e&63).
 template <int KIND, int W>
 struct SegGeo {
     static constexpr int F4 = KIND == SEG_HEAD ? 32 : W * 8;     // float4 per block
-    static constexpr int ITERS = (F4 + 255) / 256;
+    static constexpr int ITERS = (F4 + kThreads - 1) / kThreads;
     __device__ static __forceinline__ int j(int tid) { return KIND == SEG_HEAD ? tid : (tid & 31); }
     // column of float4 #i of thread tid
     __device__ static __forceinline__ int c(int tid, int i) {
-        const int h = (tid >> 5) & 1, w = tid >> 6;
-        if constexpr (KIND == SEG_ACC) return 32 * i + 8 * w + 4 * h;          // t = i, q = w
-        else if constexpr (KIND == SEG_PE) return 32 * h + 16 * i + 4 * w;     // gq = 4i + w
-        else if constexpr (KIND == SEG_DPE) return 16 * h + 4 * w;             // gq = w
+        const int h = (tid >> 5) & 1, w = (tid >> 6) & 3, hi = tid >> 8;
+        if constexpr (KIND == SEG_ACC) return 32 * (2 * i + hi) + 8 * w + 4 * h;   // t = 2i+hi, q = w
+        else if constexpr (KIND == SEG_PE) return 32 * h + 4 * (8 * i + 4 * hi + w);  // gq = 8i+4hi+w
+        else if constexpr (KIND == SEG_DPE) return 16 * h + 4 * w;               // gq = w (hi = 0)
         else return 0;
     }
 };
@@ -99,9 +102,10 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
     constexpr int MT = (WA / WM + 31) / 32, NT = (WB / WN + 31) / 32;
     constexpr int M = WA, N = WB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool active = wave < WM * WN;          // waves beyond the grid only stage
     const int mi = wave / WN, ni = wave % WN;
     const int m0 = 32 * MT * mi, n0 = 32 * NT * ni;
-    const bool do_bias = ni == 0;
+    const bool do_bias = active && ni == 0;
 
     f32x16 acc[MT][NT];
 #pragma unroll
@@ -120,9 +124,9 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
         const f32x4* pa = reinterpret_cast<const f32x4*>(T.a.base) + (size_t)blk * GA::F4 + tid;
         const f32x4* pb = reinterpret_cast<const f32x4*>(T.b.base) + (size_t)blk * GB::F4 + tid;
 #pragma unroll
-        for (int i = 0; i < GA::ITERS; ++i) if (ta) ra[i] = pa[256 * i];
+        for (int i = 0; i < GA::ITERS; ++i) if (ta) ra[i] = pa[kThreads * i];
 #pragma unroll
-        for (int i = 0; i < GB::ITERS; ++i) if (tb) rb[i] = pb[256 * i];
+        for (int i = 0; i < GB::ITERS; ++i) if (tb) rb[i] = pb[kThreads * i];
     };
     // write the staged block to LDS; samples >= n of the tail block become 0
     auto store = [&](int buf, int blk) {
@@ -170,6 +174,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
 #pragma unroll
                 for (int i = 0; i < MT; ++i) bsum[i] += av[p][i];
         };
+        if (active) {
         rd(0, 0);
 #pragma unroll
         for (int kk = 0; kk < 16; kk += 2) {
@@ -180,9 +185,11 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
             __builtin_amdgcn_sched_barrier(0);
             mm(1);
         }
+        }
         if (st + 1 < nst) store(buf ^ 1, b0 + st + 1);
         __syncthreads();
     }
+    if (!active) return;
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -201,7 +208,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
     }
 }
 
-__global__ void __launch_bounds__(256, 1) wgrad_kernel(WgArgs a) {
+__global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[2 * 2 * 32 * kRow];   // 130 KiB
     int t = 0;
 #pragma unroll 1
@@ -212,19 +219,20 @@ __global__ void __launch_bounds__(256, 1) wgrad_kernel(WgArgs a) {
     const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
     float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
     // task shapes (see nr_wgrad's task list); wave-uniform
+    // (WM, WN) = wave grid over the task's output (<= 8 waves; 128 accumulators max)
     switch (__builtin_amdgcn_readfirstlane(t)) {
         case 0: case 4:
-            wgrad_body<SEG_ACC, 256, SEG_PE, 64, 4, 1>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
         case 10:
-            wgrad_body<SEG_ACC, 128, SEG_ACC, 256, 2, 2>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 128, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
         case 11:
             wgrad_body<SEG_ACC, 128, SEG_DPE, 32, 4, 1>(a, T, b0, b1, lds, slab); break;
         case 12:
-            wgrad_body<SEG_HEAD, 4, SEG_ACC, 256, 1, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_HEAD, 4, SEG_ACC, 256, 1, 8>(a, T, b0, b1, lds, slab); break;
         case 13:
             wgrad_body<SEG_HEAD, 4, SEG_ACC, 128, 1, 4>(a, T, b0, b1, lds, slab); break;
         default:
-            wgrad_body<SEG_ACC, 256, SEG_ACC, 256, 2, 2>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
     }
 }
 
@@ -306,10 +314,10 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
     const WgSeg dzdir = acc(GD + nr_gd_dzdir(nb), 128);
     // (a, b, wm, wn); task order fixes wgrad_dest / wgrad_bias_dest
     const WgTask tasks[kTasks] = {
-        {DZ(0), pe, 4, 1}, {DZ(1), H(0), 2, 2}, {DZ(2), H(1), 2, 2}, {DZ(3), H(2), 2, 2},
-        {DZ(4), pe, 4, 1}, {DZ(4), H(3), 2, 2}, {DZ(5), H(4), 2, 2}, {DZ(6), H(5), 2, 2},
-        {DZ(7), H(6), 2, 2}, {DZ(8), H(7), 2, 2}, {dzdir, feat, 2, 2}, {dzdir, dpe, 4, 1},
-        {head, H(7), 1, 4}, {head, hdir, 1, 4},
+        {DZ(0), pe, 8, 1}, {DZ(1), H(0), 2, 4}, {DZ(2), H(1), 2, 4}, {DZ(3), H(2), 2, 4},
+        {DZ(4), pe, 8, 1}, {DZ(4), H(3), 2, 4}, {DZ(5), H(4), 2, 4}, {DZ(6), H(5), 2, 4},
+        {DZ(7), H(6), 2, 4}, {DZ(8), H(7), 2, 4}, {dzdir, feat, 2, 4}, {dzdir, dpe, 4, 1},
+        {head, H(7), 1, 8}, {head, hdir, 1, 4},
     };
     WgArgs a{};
     // per-block cost of a task's workgroup, in cycles: its waves' MFMA time,
@@ -320,7 +328,8 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
         a.task[t] = tasks[t];
         const int mt = (tasks[t].a.width / tasks[t].wm + 31) / 32;
         const int nt = (tasks[t].b.width / tasks[t].wn + 31) / 32;
-        const int64_t mfma = 16 * mt * nt * 64;
+        // MFMA cycles of the busiest SIMD (two waves per SIMD when > 4 are active)
+        const int64_t mfma = 16 * mt * nt * 64 * (tasks[t].wm * tasks[t].wn > 4 ? 2 : 1);
         const int64_t bytes = (int64_t)(tasks[t].a.width + tasks[t].b.width) * 32 * 4;
         cost[t] = std::max<int64_t>(mfma, bytes / 8) + 512;
         tot += cost[t];
@@ -343,7 +352,7 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
     a.nb = (int)nb;
     a.n = (int)n;
     a.slab = workspace;
-    wgrad_kernel<<<a.wg_start[kTasks], 256, 0, st>>>(a);
+    wgrad_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     NR_LAUNCH_CHECK("nr_wgrad");
     dim3 rg((256 * 256 + 256 + 255) / 256, kTasks);
     wgrad_reduce_kernel<<<rg, 256, 0, st>>>(a, grad_flat);
