@@ -23,7 +23,9 @@ constexpr int kTasks = 14;
 constexpr int kTargetWG = 760;   // ~3 rounds of one workgroup per CU (short tail)
 constexpr int kThreads = 512;    // 8 waves: two per SIMD, so one wave's staging and
                                  // barrier time overlaps its partner's MFMAs
-constexpr int kRow = 260;        // LDS row stride (floats)
+constexpr int kCol = 36;         // LDS column stride (floats): [column][32 samples + 4 pad]
+constexpr int kBufA = 256 * kCol;  // one operand region
+constexpr int kBuf = 2 * kBufA;    // one buffer = A + B regions
 
 enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
 
@@ -128,20 +130,30 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
 #pragma unroll
         for (int i = 0; i < GB::ITERS; ++i) if (tb) rb[i] = pb[kThreads * i];
     };
-    // write the staged block to LDS; samples >= n of the tail block become 0
+    // write the staged block to LDS as [column][sample] (4 ds_write_b32 per
+    // float4; lanes are consecutive samples -> conflict-free); samples >= n of
+    // the tail block become 0
     auto store = [&](int buf, int blk) {
         const int nval = a.n - blk * 32;
         const bool ka = ja < nval, kb = jb < nval;
-        float* la = lds + buf * (2 * 32 * kRow) + ja * kRow;
-        float* lb = lds + buf * (2 * 32 * kRow) + 32 * kRow + jb * kRow;
+        float* la = lds + buf * kBuf + ja;
+        float* lb = lds + buf * kBuf + kBufA + jb;
         if (ta)
 #pragma unroll
-            for (int i = 0; i < GA::ITERS; ++i)
-                *reinterpret_cast<f32x4*>(la + GA::c(tid, i)) = ka ? ra[i] : f32x4{};
+            for (int i = 0; i < GA::ITERS; ++i) {
+                const f32x4 v = ka ? ra[i] : f32x4{};
+                const int c = GA::c(tid, i);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) la[(c + e) * kCol] = v[e];
+            }
         if (tb)
 #pragma unroll
-            for (int i = 0; i < GB::ITERS; ++i)
-                *reinterpret_cast<f32x4*>(lb + GB::c(tid, i)) = kb ? rb[i] : f32x4{};
+            for (int i = 0; i < GB::ITERS; ++i) {
+                const f32x4 v = kb ? rb[i] : f32x4{};
+                const int c = GB::c(tid, i);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) lb[(c + e) * kCol] = v[e];
+            }
     };
 
     const int nst = b1 - b0;
@@ -155,36 +167,42 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
     for (int st = 0; st < nst; ++st) {
         const int buf = st & 1;
         if (st + 1 < nst) load(b0 + st + 1);
-        const float* la = lds + buf * (2 * 32 * kRow) + h * kRow + m0 + col;
-        const float* lb = lds + buf * (2 * 32 * kRow) + 32 * kRow + h * kRow + n0 + col;
-        // operands double-buffered one k-step ahead (LDS latency off the MFMA path)
-        float av[2][MT], bv[2][NT];
-        auto rd = [&](int kk, int p) {
-#pragma unroll
-            for (int i = 0; i < MT; ++i) av[p][i] = la[2 * kk * kRow + 32 * i];
-#pragma unroll
-            for (int j = 0; j < NT; ++j) bv[p][j] = lb[2 * kk * kRow + 32 * j];
-        };
-        auto mm = [&](int p) {
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int j = 0; j < NT; ++j) acc[i][j] = nr_mfma32(av[p][i], bv[p][j], acc[i][j]);
-            if (do_bias)
-#pragma unroll
-                for (int i = 0; i < MT; ++i) bsum[i] += av[p][i];
-        };
+        // k-step kk pairs samples kk (lane half 0) and 16 + kk (half 1): a lane's
+        // 16 samples of one column are contiguous -> 4 ds_read_b128 per column
+        const float* la = lds + buf * kBuf + (m0 + col) * kCol + 16 * h;
+        const float* lb = lds + buf * kBuf + kBufA + (n0 + col) * kCol + 16 * h;
         if (active) {
-        rd(0, 0);
+            f32x4 av[2][MT], bv[2][NT];
+            auto rd = [&](int q, int p) {   // samples 4q..4q+3 of this lane half
 #pragma unroll
-        for (int kk = 0; kk < 16; kk += 2) {
-            rd(kk + 1, 1);
+                for (int i = 0; i < MT; ++i) av[p][i] = *reinterpret_cast<const f32x4*>(la + 32 * i * kCol + 4 * q);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) bv[p][j] = *reinterpret_cast<const f32x4*>(lb + 32 * j * kCol + 4 * q);
+            };
+            auto mm = [&](int p) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+#pragma unroll
+                        for (int j = 0; j < NT; ++j)
+                            acc[i][j] = nr_mfma32(av[p][i][e], bv[p][j][e], acc[i][j]);
+#pragma unroll
+                    for (int i = 0; i < MT; ++i) bsum[i] += av[p][i][e];
+                }
+            };
+            rd(0, 0);
+            rd(1, 1);
             __builtin_amdgcn_sched_barrier(0);
             mm(0);
-            if (kk + 2 < 16) rd(kk + 2, 0);
+            rd(2, 0);
             __builtin_amdgcn_sched_barrier(0);
             mm(1);
-        }
+            rd(3, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mm(0);
+            __builtin_amdgcn_sched_barrier(0);
+            mm(1);
         }
         if (st + 1 < nst) store(buf ^ 1, b0 + st + 1);
         __syncthreads();
@@ -209,7 +227,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
 }
 
 __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
-    __shared__ __attribute__((aligned(16))) float lds[2 * 2 * 32 * kRow];   // 130 KiB
+    __shared__ __attribute__((aligned(16))) float lds[2 * kBuf];   // 144 KiB
     int t = 0;
 #pragma unroll 1
     while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
