@@ -69,6 +69,7 @@ struct WgTask {
     int wm, wn;          // wave grid (wm * wn == 4)
     int G;               // workgroups
     int64_t slab;        // slab offset (floats) of workgroup 0
+    int id;              // task id: selects the gradient destination and the kernel shape
 };
 
 struct WgArgs {
@@ -238,7 +239,7 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
     // task shapes (see nr_wgrad's task list); wave-uniform
     // (WM, WN) = wave grid over the task's output (<= 8 waves; 128 accumulators max)
-    switch (__builtin_amdgcn_readfirstlane(t)) {
+    switch (__builtin_amdgcn_readfirstlane(T.id)) {
         case 0: case 4:
             wgrad_body<SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
         case 10:
@@ -292,7 +293,7 @@ __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     const int nw = M * N, sz = nw + M;
     if (e >= sz) return;
-    const int dst = e < nw ? wgrad_dest(t, e / N, e % N) : wgrad_bias_dest(t, e - nw);
+    const int dst = e < nw ? wgrad_dest(T.id, e / N, e % N) : wgrad_bias_dest(T.id, e - nw);
     if (dst < 0) return;
     const float* p = a.slab + T.slab + e;
     float s = 0.f;
@@ -305,7 +306,7 @@ __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
 NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
     (void)n;
     // upper bound of sum_t G_t * (M_t N_t + M_t) for the task list below
-    return (int64_t)(kTargetWG + kTasks) * (256 * 256 + 256) * sizeof(float);
+    return (int64_t)(3 * kTargetWG + kTasks) * (256 * 256 + 256) * sizeof(float);
 }
 
 NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
@@ -338,34 +339,43 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
         {head, H(7), 1, 8}, {head, hdir, 1, 4},
     };
     WgArgs a{};
-    // per-block cost of a task's workgroup, in cycles: its waves' MFMA time,
-    // or the staging of (M + N) x 32 floats at ~8 B/cycle per CU, plus a
-    // fixed barrier/LDS-store overhead
+    // per-block cost of a task's workgroup, in cycles: the MFMA time of its
+    // busiest SIMD, or the staging of (M + N) x 32 floats at ~8 B/cycle per CU,
+    // plus a fixed barrier/LDS-store overhead
     int64_t cost[kTasks], tot = 0;
     for (int t = 0; t < kTasks; ++t) {
-        a.task[t] = tasks[t];
         const int mt = (tasks[t].a.width / tasks[t].wm + 31) / 32;
         const int nt = (tasks[t].b.width / tasks[t].wn + 31) / 32;
-        // MFMA cycles of the busiest SIMD (two waves per SIMD when > 4 are active)
         const int64_t mfma = 16 * mt * nt * 64 * (tasks[t].wm * tasks[t].wn > 4 ? 2 : 1);
         const int64_t bytes = (int64_t)(tasks[t].a.width + tasks[t].b.width) * 32 * 4;
         cost[t] = std::max<int64_t>(mfma, bytes / 8) + 512;
         tot += cost[t];
     }
+    // dispatch order: the heavy 256x256 tasks first; the small, memory-bound
+    // tasks last and split ~3x finer, so their short workgroups fill the tail
+    // of the final round
+    int order[kTasks], no = 0;
+    for (int pass = 0; pass < 2; ++pass)
+        for (int t = 0; t < kTasks; ++t)
+            if ((cost[t] >= 16384) == (pass == 0)) order[no++] = t;
     a.wg_start[0] = 0;
     int64_t slab = 0;
-    // diagnostic: NR_WGRAD_TASKMASK limits the launch to a subset of tasks (the
-    // kernel code is unchanged; gradients of the other tasks are then stale)
+    // diagnostic: NR_WGRAD_TASKMASK limits the launch to a subset of task ids
+    // (the kernel code is unchanged; gradients of the other tasks are then stale)
     static const long long tmask =
         getenv("NR_WGRAD_TASKMASK") ? strtoll(getenv("NR_WGRAD_TASKMASK"), nullptr, 0) : -1;
-    for (int t = 0; t < kTasks; ++t) {
-        int64_t g = (kTargetWG * cost[t] + tot - 1) / tot;   // per-workgroup work <= target
+    for (int k = 0; k < kTasks; ++k) {
+        const int t = order[k];
+        const int split = cost[t] >= 16384 ? 1 : 3;
+        int64_t g = split * ((kTargetWG * cost[t] + tot - 1) / tot);
         g = std::max<int64_t>(1, std::min<int64_t>(g, nb));
         if (!((tmask >> t) & 1)) g = 0;
-        a.task[t].G = (int)g;
-        a.task[t].slab = slab;
-        slab += (int64_t)g * (tasks[t].a.width * tasks[t].b.width + tasks[t].a.width);
-        a.wg_start[t + 1] = a.wg_start[t] + (int)g;
+        a.task[k] = tasks[t];
+        a.task[k].id = t;
+        a.task[k].G = (int)g;
+        a.task[k].slab = slab;
+        slab += g * (tasks[t].a.width * tasks[t].b.width + tasks[t].a.width);
+        a.wg_start[k + 1] = a.wg_start[k] + (int)g;
     }
     a.nb = (int)nb;
     a.n = (int)n;
