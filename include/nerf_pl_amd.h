@@ -59,6 +59,13 @@ int nr_mlp_fwd(const float* packed_fwd, const float* rays, const float* z, int64
                int samples_per_ray, const float* x, int xstride, int sigma_only, float* out,
                float* save, void* stream);
 
+/* Dense sigma query (extract_color_mesh.py:114-137, the marching-cubes grid):
+ * sigma_out (n) = NeRF sigma head at points pts (n,3) -- the sigma-only fused
+ * kernel with the positional encoding computed in-kernel (sigma does not
+ * depend on the view direction, nerf.py:112). */
+int nr_mlp_sigma_points(const float* packed_fwd, const float* pts, int64_t n, float* sigma_out,
+                        void* stream);
+
 /* MLP backward, data-gradient chain (autograd of nerf.py:83-124): from
  * g_out (n,4) = d[rgb, sigma] writes every layer's pre-activation gradient to
  * grad_ws (n*nr_layout_query(4) floats). */
@@ -78,19 +85,21 @@ int nr_coarse_z(const float* rays, const float* tlin, int64_t n_rays, int n_samp
                 int use_disp, float perturb, const float* u, uint64_t seed, float* z_out,
                 void* stream);
 
-/* Volume compositing (rendering.py:169-198), one wave per ray.  raw rows of
- * raw_stride floats with rgb at 0..2 and sigma at sig_col.  noise: (n_rays,S)
- * replay of torch.randn or NULL.  Writes weights (n_rays,S), opacity, and unless
- * weights_only rgb (n_rays,3) and depth. */
+/* Volume compositing (rendering.py:169-198; sigma-only variant
+ * rendering_shadows.py:164-198), one wave per ray.  raw rows of raw_stride
+ * floats with sigma at sig_col and, when rgb != NULL, rgb at 0..2.  noise:
+ * (n_rays,S) replay of torch.randn or NULL.  Writes weights (n_rays,S),
+ * opacity, and unless weights_only depth and (if rgb != NULL) rgb (n_rays,3). */
 int nr_composite_fwd(const float* raw, int raw_stride, int sig_col, const float* z,
                      const float* rays, const float* noise, float noise_std, uint64_t seed,
                      int rng_stream, int64_t n_rays, int n_samples, int white_back,
                      int weights_only, float* rgb, float* depth, float* opacity,
                      float* weights, void* stream);
 
-/* Autograd of the compositing step: d(rgb, depth, opacity) -> g_raw (n_rays*S, 4)
- * = d[rgb_i, sigma_i].  Any gradient pointer may be NULL (zero). */
-int nr_composite_bwd(const float* raw, const float* z, const float* rays, const float* noise,
+/* Autograd of the compositing step: d(rgb, depth, opacity) -> g_raw, rows of
+ * raw_stride floats like raw: d sigma_i at sig_col and, when raw_stride == 4,
+ * d rgb_i at 0..2.  Any gradient pointer may be NULL (zero). */
+int nr_composite_bwd(const float* raw, int raw_stride, int sig_col, const float* z, const float* rays, const float* noise,
                      float noise_std, uint64_t seed, int rng_stream, int64_t n_rays,
                      int n_samples, int white_back, const float* g_rgb, const float* g_depth,
                      const float* g_opacity, float* g_raw, void* stream);
@@ -103,6 +112,33 @@ int nr_composite_bwd(const float* raw, const float* z, const float* rays, const 
 int nr_sample_pdf(const float* weights, int n_samples, const float* rays,
                   const float* z_coarse, const float* u, const float* jitter, uint64_t seed,
                   int64_t n_rays, int n_importance, float* z_pdf, float* z_fine, void* stream);
+
+/* ---- shadow mapping (config 5: train_efficient_sm.py) ---------------------
+ * get_normed_w column 3 (efficient_shadow_mapping.py:41-58): out (n) =
+ * depth / (|camera @ pixel| + 1e-5); camera (3,3) row-major, pixels (n,3). */
+int nr_sm_normed_depth(const float* camera, const float* pixels, const float* depth, int64_t n,
+                       float* out, void* stream);
+
+/* efficient_sm's shadow maps (rendering_shadows.py:359-482 with
+ * efficient_shadow_mapping.py:19-130): for camera rays with pixels (n,3) and
+ * depth (n), per-ray eye (n,3) and camera (n,3,3) (per_ray=1; runs of equal
+ * eye position are split exactly like the reference's torch.equal loop and use
+ * the run's first camera) or one eye/camera for all (per_ray=0), the light
+ * camera (3,3) + eye (3) and the light's normed depth map light_w (res_w*res_h)
+ * -> out (n,3) = shadow value + out_eps.  method 1: clip(max(d/delta, epsilon));
+ * method 2: per-run min-max normalisation (+ sigmoid).  workspace:
+ * nr_sm_workspace_bytes(n); keep it for nr_sm_backward. */
+int64_t nr_sm_workspace_bytes(int64_t n);
+int nr_sm_forward(const float* pixels, const float* depth, const float* eye, const float* cameras,
+                  int per_ray, const float* light_camera, const float* light_eye,
+                  const float* light_w, int res_w, int res_h, int method, float delta,
+                  float epsilon, int sigmoid, float out_eps, int64_t n, void* workspace,
+                  float* out, void* stream);
+/* Autograd of nr_sm_forward w.r.t. the camera depth: g_out (n,3) -> g_depth (n).
+ * The light map is treated as a constant (train_efficient_sm.py renders it
+ * under no_grad unless --grad_on_light). */
+int nr_sm_backward(const float* g_out, void* workspace, int method, float delta, float epsilon,
+                   int sigmoid, int64_t n, float* g_depth, void* stream);
 
 /* Test hook: one v_mfma_f32_32x32x2_f32 on A (32x2), B (2x32) -> D (32x32). */
 int nr_probe_mfma32(const float* a, const float* b, float* d, void* stream);

@@ -20,13 +20,20 @@ _f = ctypes.c_float
 # name -> argtypes; every entry returns int (0 = ok) unless listed in _RESTYPES
 SIGNATURES = {
     "nr_mlp_fwd": [_p, _p, _p, _i64, _i, _p, _i, _i, _p, _p, _p],
+    "nr_mlp_sigma_points": [_p, _p, _i64, _p, _p],
     "nr_mlp_bwd": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
+    "nr_sm_workspace_bytes": [_i64],
     "nr_wgrad": [_p, _p, _i64, _p, _p, _p],
     "nr_coarse_z": [_p, _p, _i64, _i, _i, _f, _p, _u64, _p, _p],
     "nr_composite_fwd": [_p, _i, _i, _p, _p, _p, _f, _u64, _i, _i64, _i, _i, _i, _p, _p, _p,
                          _p, _p],
-    "nr_composite_bwd": [_p, _p, _p, _p, _f, _u64, _i, _i64, _i, _i, _p, _p, _p, _p, _p],
+    "nr_composite_bwd": [_p, _i, _i, _p, _p, _p, _f, _u64, _i, _i64, _i, _i, _p, _p, _p, _p,
+                         _p],
+    "nr_sm_normed_depth": [_p, _p, _p, _i64, _p, _p],
+    "nr_sm_forward": [_p, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _f, _f, _i, _f, _i64, _p, _p,
+                      _p],
+    "nr_sm_backward": [_p, _p, _i, _f, _f, _i, _i64, _p, _p],
     "nr_sample_pdf": [_p, _i, _p, _p, _p, _p, _u64, _i64, _i, _p, _p, _p],
     "nr_embed": [_p, _i64, _i, _p, _p],
     "nr_pack": [_p, _p, _i64, _p, _p],
@@ -34,7 +41,8 @@ SIGNATURES = {
     "nr_layout_query": [_i],
     "nr_last_error": [],
 }
-_RESTYPES = {"nr_layout_query": _i64, "nr_wgrad_workspace_bytes": _i64, "nr_last_error": ctypes.c_char_p}
+_RESTYPES = {"nr_layout_query": _i64, "nr_wgrad_workspace_bytes": _i64,
+             "nr_sm_workspace_bytes": _i64, "nr_last_error": ctypes.c_char_p}
 
 _lib = None
 

@@ -92,8 +92,11 @@ __device__ __forceinline__ void pe_gather(float (&pe)[KS], const float* __restri
     for (int g = 2 + 2 * NP; g < KS; ++g) pe[g] = 0.f;
 }
 
+enum FwdMode { FWD_RAYS = 0, FWD_EMB = 1, FWD_PTS = 2 };
+
 struct FwdArgs {
     const float* packed;
+    const float* pts;    // (n, 3) points (FWD_PTS: dense sigma query)
     const float* rays;   // (n_rays, 8) [o, d, near, far]
     const float* z;      // (n) depths, sample-major (ray*spr + k)
     const float* x;      // (n, xstride) embedded input (EMB path)
@@ -104,8 +107,9 @@ struct FwdArgs {
     float* save;         // saved activations (training) or nullptr
 };
 
-template <bool EMB, bool SIGMA_ONLY>
+template <int MODE, bool SIGMA_ONLY>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
+    constexpr bool EMB = MODE == FWD_EMB;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
@@ -134,6 +138,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     if constexpr (EMB) {
         xrow = a.x + (size_t)s * a.xstride;
         px = py = pz = 0.f;
+    } else if constexpr (MODE == FWD_PTS) {
+        px = a.pts[(size_t)s * 3 + 0];
+        py = a.pts[(size_t)s * 3 + 1];
+        pz = a.pts[(size_t)s * 3 + 2];
     } else {
         const int ray = s / a.spr;
         const float* r = a.rays + (size_t)ray * 8;
@@ -281,16 +289,31 @@ NR_API int nr_mlp_fwd(const float* packed, const float* rays, const float* z, in
     } else {
         NR_REQUIRE(rays && z && samples_per_ray > 0, "nr_mlp_fwd: rays/z/samples_per_ray");
     }
-    FwdArgs a{packed, rays, z, x, (int)n, samples_per_ray, xstride, out, save};
+    FwdArgs a{packed, nullptr, rays, z, x, (int)n, samples_per_ray, xstride, out, save};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
     hipStream_t st = (hipStream_t)stream;
     if (emb) {
-        if (sigma_only) mlp_fwd_kernel<true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
-        else mlp_fwd_kernel<true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+        if (sigma_only) mlp_fwd_kernel<FWD_EMB, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_fwd_kernel<FWD_EMB, false><<<blocks, 64 * kWaves, 0, st>>>(a);
     } else {
-        if (sigma_only) mlp_fwd_kernel<false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
-        else mlp_fwd_kernel<false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+        if (sigma_only) mlp_fwd_kernel<FWD_RAYS, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_fwd_kernel<FWD_RAYS, false><<<blocks, 64 * kWaves, 0, st>>>(a);
     }
     NR_LAUNCH_CHECK("nr_mlp_fwd");
+    return 0;
+}
+
+// Dense sigma query at points (extract_color_mesh.py:114-137): sigma-only MLP on
+// (n,3) points with the positional encoding computed in-kernel.
+NR_API int nr_mlp_sigma_points(const float* packed_fwd, const float* pts, int64_t n,
+                               float* sigma_out, void* stream) {
+    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_sigma_points: n out of range");
+    if (n == 0) return 0;
+    NR_REQUIRE(packed_fwd && pts && sigma_out, "nr_mlp_sigma_points: null pointer");
+    NR_REQUIRE(((uintptr_t)packed_fwd & 15) == 0, "nr_mlp_sigma_points: packed must be 16-byte aligned");
+    FwdArgs a{packed_fwd, pts, nullptr, nullptr, nullptr, (int)n, 1, 0, sigma_out, nullptr};
+    const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
+    mlp_fwd_kernel<FWD_PTS, true><<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
+    NR_LAUNCH_CHECK("nr_mlp_sigma_points");
     return 0;
 }

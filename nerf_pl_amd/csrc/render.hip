@@ -133,10 +133,12 @@ __global__ void composite_fwd_kernel(CompArgs a) {
             a.weights[base + i] = w;
             acc_w += w;
             if (!a.weights_only) {
-                const float* rr = a.raw + (base + i) * a.raw_stride;
-                acc_r = fmaf(w, rr[0], acc_r);
-                acc_g = fmaf(w, rr[1], acc_g);
-                acc_b = fmaf(w, rr[2], acc_b);
+                if (a.rgb) {
+                    const float* rr = a.raw + (base + i) * a.raw_stride;
+                    acc_r = fmaf(w, rr[0], acc_r);
+                    acc_g = fmaf(w, rr[1], acc_g);
+                    acc_b = fmaf(w, rr[2], acc_b);
+                }
                 acc_d = fmaf(w, zi, acc_d);
             }
         }
@@ -150,9 +152,11 @@ __global__ void composite_fwd_kernel(CompArgs a) {
     acc_d = wave_sum(acc_d);
     if (lane == 0) {
         const float bg = a.white_back ? 1.f - acc_w : 0.f;   // rendering.py:195-196
-        a.rgb[(size_t)ray * 3 + 0] = acc_r + bg;
-        a.rgb[(size_t)ray * 3 + 1] = acc_g + bg;
-        a.rgb[(size_t)ray * 3 + 2] = acc_b + bg;
+        if (a.rgb) {
+            a.rgb[(size_t)ray * 3 + 0] = acc_r + bg;
+            a.rgb[(size_t)ray * 3 + 1] = acc_g + bg;
+            a.rgb[(size_t)ray * 3 + 2] = acc_b + bg;
+        }
         a.depth[ray] = acc_d;
         a.opacity[ray] = acc_w;
     }
@@ -167,11 +171,11 @@ __global__ void composite_fwd_kernel(CompArgs a) {
 //   dc_i  = w_i * drgb
 // ---------------------------------------------------------------------------
 struct CompBwdArgs {
-    const float* raw; const float* z; const float* rays; const float* noise;
+    const float* raw; int raw_stride; int sig_col; const float* z; const float* rays; const float* noise;
     float noise_std; uint64_t seed; uint32_t stream;
     int n_rays, S, white_back;
     const float* g_rgb; const float* g_depth; const float* g_opacity;
-    float* g_raw;   // (n_rays*S, 4)
+    float* g_raw;   // (n_rays*S, raw_stride)
 };
 
 __global__ void composite_bwd_kernel(CompBwdArgs a) {
@@ -204,7 +208,7 @@ __global__ void composite_bwd_kernel(CompBwdArgs a) {
                 const float zj = a.z[base + j];
                 const float delta = j + 1 < S ? nr_mul(nr_sub(a.z[base + j + 1], zj), dn)
                                               : nr_mul(1e10f, dn);
-                const float al = alpha_of(a.raw[(base + j) * 4 + 3],
+                const float al = alpha_of(a.raw[(base + j) * a.raw_stride + a.sig_col],
                                           sample_noise(a.noise, a.noise_std, a.seed, a.stream,
                                                        base + j), delta);
                 fac = nr_add(1.f - al, 1e-10f);
@@ -217,11 +221,12 @@ __global__ void composite_bwd_kernel(CompBwdArgs a) {
         if (v) {
             zi = a.z[base + i];
             delta = i + 1 < S ? nr_mul(nr_sub(a.z[base + i + 1], zi), dn) : nr_mul(1e10f, dn);
-            const float* rr = a.raw + (base + i) * 4;
-            cr = rr[0]; cg = rr[1]; cb = rr[2];
+            const float* rr = a.raw + (base + i) * a.raw_stride;
+            if (a.raw_stride == 4) { cr = rr[0]; cg = rr[1]; cb = rr[2]; }
+            const float sg = rr[a.sig_col];
             const float nz = sample_noise(a.noise, a.noise_std, a.seed, a.stream, base + i);
-            srel = nr_add(rr[3], nz);
-            alpha = alpha_of(rr[3], nz, delta);
+            srel = nr_add(sg, nz);
+            alpha = alpha_of(sg, nz, delta);
         }
         const float fac = v ? nr_add(1.f - alpha, 1e-10f) : 1.f;
         const double incl = wave_incl_prod((double)fac, lane);
@@ -244,8 +249,12 @@ __global__ void composite_bwd_kernel(CompBwdArgs a) {
             const float da = T * (dw - Ri);
             const float rl = srel > 0.f ? srel : 0.f;
             const float dsig = srel > 0.f ? da * expf(nr_mul(-delta, rl)) * delta : 0.f;
-            f32x4 o = {w * gr, w * gg, w * gb, dsig};
-            *reinterpret_cast<f32x4*>(a.g_raw + (base + i) * 4) = o;
+            if (a.raw_stride == 4) {
+                f32x4 o = {w * gr, w * gg, w * gb, dsig};
+                *reinterpret_cast<f32x4*>(a.g_raw + (base + i) * 4) = o;
+            } else {
+                a.g_raw[(base + i) * a.raw_stride + a.sig_col] = dsig;
+            }
         }
         Rcarry = Rnext;
     }
@@ -357,7 +366,10 @@ NR_API int nr_composite_fwd(const float* raw, int raw_stride, int sig_col, const
     NR_REQUIRE(n_rays >= 0 && n_samples > 0, "nr_composite_fwd: bad sizes");
     if (n_rays == 0) return 0;
     NR_REQUIRE(raw && z && rays && opacity && weights, "nr_composite_fwd: null pointer");
-    NR_REQUIRE(weights_only || (rgb && depth), "nr_composite_fwd: null rgb/depth");
+    NR_REQUIRE(weights_only || depth, "nr_composite_fwd: null depth");
+    NR_REQUIRE(sig_col >= 0 && sig_col < raw_stride && (!rgb || raw_stride >= 4),
+               "nr_composite_fwd: bad raw layout (stride %d, sigma column %d)", raw_stride,
+               sig_col);
     CompArgs a{raw, raw_stride, sig_col, z, rays, noise, noise_std, seed, (uint32_t)rng_stream,
                (int)n_rays, n_samples, white_back, weights_only, rgb, depth, opacity, weights};
     const int wpb = 4;
@@ -367,7 +379,8 @@ NR_API int nr_composite_fwd(const float* raw, int raw_stride, int sig_col, const
     return 0;
 }
 
-NR_API int nr_composite_bwd(const float* raw, const float* z, const float* rays,
+NR_API int nr_composite_bwd(const float* raw, int raw_stride, int sig_col, const float* z,
+                            const float* rays,
                             const float* noise, float noise_std, uint64_t seed, int rng_stream,
                             int64_t n_rays, int n_samples, int white_back, const float* g_rgb,
                             const float* g_depth, const float* g_opacity, float* g_raw,
@@ -375,8 +388,11 @@ NR_API int nr_composite_bwd(const float* raw, const float* z, const float* rays,
     NR_REQUIRE(n_rays >= 0 && n_samples > 0, "nr_composite_bwd: bad sizes");
     if (n_rays == 0) return 0;
     NR_REQUIRE(raw && z && rays && g_raw, "nr_composite_bwd: null pointer");
-    NR_REQUIRE(((uintptr_t)g_raw & 15) == 0, "nr_composite_bwd: g_raw must be 16-byte aligned");
-    CompBwdArgs a{raw, z, rays, noise, noise_std, seed, (uint32_t)rng_stream, (int)n_rays,
+    NR_REQUIRE(raw_stride == 4 ? sig_col == 3 : (raw_stride == 1 && sig_col == 0),
+               "nr_composite_bwd: raw rows must be [rgb, sigma] or [sigma]");
+    NR_REQUIRE(raw_stride != 4 || ((uintptr_t)g_raw & 15) == 0,
+               "nr_composite_bwd: g_raw must be 16-byte aligned");
+    CompBwdArgs a{raw, raw_stride, sig_col, z, rays, noise, noise_std, seed, (uint32_t)rng_stream, (int)n_rays,
                   n_samples, white_back, g_rgb, g_depth, g_opacity, g_raw};
     const int wpb = 4;
     composite_bwd_kernel<<<(unsigned)((n_rays + wpb - 1) / wpb), 64 * wpb, 0,

@@ -88,6 +88,15 @@ def mlp_forward(packed: torch.Tensor, *, rays=None, z=None, samples_per_ray=0, x
     return out, sv
 
 
+def sigma_points(packed, pts):
+    """sigma (n,) of the fused sigma-only MLP at points (n,3)."""
+    pts = _dev(pts, "pts", 3)
+    out = torch.empty(pts.shape[0], device=pts.device)
+    call("nr_mlp_sigma_points", ptr(packed), ptr(pts), pts.shape[0], ptr(out),
+         stream_of(pts.device))
+    return out
+
+
 def coarse_z(rays, n_samples, use_disp, perturb, u=None, seed=0):
     rays = _dev(rays, "rays", 8)
     n_rays = rays.shape[0]
@@ -100,14 +109,15 @@ def coarse_z(rays, n_samples, use_disp, perturb, u=None, seed=0):
 
 def composite_forward(raw, z, rays, noise, noise_std, seed, rng_stream, white_back,
                       weights_only=False):
-    """raw (R*S, 4) [rgb, sigma] or (R*S, 1) sigma."""
+    """raw (R*S, 4) [rgb, sigma] or (R*S, 1) sigma (then rgb is None: the
+    sigma-only render of rendering_shadows.py:164-198)."""
     z = _dev(z, "z")
     n_rays, S = z.shape
     stride = raw.shape[-1]
     dev = z.device
     opac = torch.empty(n_rays, device=dev)
     w = torch.empty(n_rays, S, device=dev)
-    rgb = None if weights_only else torch.empty(n_rays, 3, device=dev)
+    rgb = None if weights_only or stride < 4 else torch.empty(n_rays, 3, device=dev)
     depth = None if weights_only else torch.empty(n_rays, device=dev)
     call("nr_composite_fwd", ptr(raw), stride, stride - 1, ptr(z), ptr(rays), ptr(noise),
          float(noise_std), seed, rng_stream, n_rays, S, int(white_back), int(weights_only),
@@ -118,8 +128,9 @@ def composite_forward(raw, z, rays, noise, noise_std, seed, rng_stream, white_ba
 def composite_backward(raw, z, rays, noise, noise_std, seed, rng_stream, white_back,
                        g_rgb, g_depth, g_opacity):
     n_rays, S = z.shape
-    g_raw = torch.empty(n_rays * S, 4, device=z.device)
-    call("nr_composite_bwd", ptr(raw), ptr(z), ptr(rays), ptr(noise), float(noise_std), seed,
+    stride = raw.shape[-1]
+    g_raw = torch.empty(n_rays * S, stride, device=z.device)
+    call("nr_composite_bwd", ptr(raw), stride, stride - 1, ptr(z), ptr(rays), ptr(noise), float(noise_std), seed,
          rng_stream, n_rays, S, int(white_back),
          ptr(None if g_rgb is None else g_rgb.contiguous()),
          ptr(None if g_depth is None else g_depth.contiguous()),

@@ -234,3 +234,25 @@ def test_sample_pdf_and_merge(case):
     # merged output is the sorted union (exact, independent of flips)
     exp = np.sort(np.concatenate([cap["z_coarse"].numpy(), z_pdf], 1), 1)
     np.testing.assert_array_equal(z_fine.cpu().numpy(), exp)
+
+
+def test_dense_sigma_grid_matches_reference_recipe():
+    """extract_color_mesh.py:114-139: embed the N^3 grid with a zero direction,
+    run the full fine NeRF, keep max(sigma,0).  The fused points kernel must
+    give the same grid (sigma does not depend on the direction)."""
+    from nerf_pl_amd import NeRF
+    from nerf_pl_amd.extract import grid_points, query_sigma, sigma_grid
+    p = O.make_params(7, sigma_bias=0.1)
+    model = NeRF().to(DEV)
+    model.load_state_dict({k: v for k, v in p.items()})
+    N = 23                                        # 12,167 points: ragged vs 128
+    rng = (-1.2, 1.2)
+    pts = grid_points(N, rng, rng, rng, "cpu")
+    x = torch.cat([O.embed(pts, 10), O.embed(torch.zeros_like(pts), 4)], 1)
+    ref = O.nerf_forward(p, x)[:, -1]
+    got = query_sigma(model, pts.to(DEV)).cpu()
+    assert (got - ref).abs().max().item() < 2e-5
+    grid = sigma_grid(model, N, rng, rng, rng).cpu()
+    assert grid.shape == (N, N, N)
+    torch.testing.assert_close(grid, torch.clamp_min(ref, 0).reshape(N, N, N), rtol=0, atol=2e-5)
+    assert query_sigma(model, torch.zeros(0, 3, device=DEV)).shape == (0,)
