@@ -1,10 +1,13 @@
 """Training-step throughput of the drop-in render_rays path on MI355X.
 
 One step = one NeRFSystem.training_step of the reference (train.py:103-117)
-on synthetic Blender-lego 400x400 rays: gather B=4096 rays per rank from an
-HBM-resident ray pool -> render_rays (64 coarse + 128 fine, perturb=1,
-noise_std=1: opt.py defaults) -> MSE(coarse)+MSE(fine) -> backward ->
-[RCCL all-reduce of the 4.77 MB gradient when N>1] -> Adam(lr=5e-4).
+on synthetic Blender-lego 400x400 rays: B=4096 rays per rank generated on the
+device from the 100 camera poses of an orbit (nr_gen_rays; an epoch-shuffled
+permutation of all 16M pixels, like the reference's shuffled DataLoader over
+its ray buffer, with the target colours gathered in the same pass) ->
+render_rays (64 coarse + 128 fine, perturb=1, noise_std=1: opt.py defaults) ->
+MSE(coarse)+MSE(fine) -> backward -> [RCCL all-reduce of the 4.77 MB gradient
+when N>1] -> Adam(lr=5e-4, eps=1e-8) as one fused launch.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -81,6 +84,8 @@ def install_timers(timer):
             return "mlp_bwd_dgrad", int(a[5])
         if name == "nr_wgrad":
             return "mlp_wgrad", int(a[2])
+        if name == "nr_adam_step":
+            return "adam", 0
         return name[3:], 0
 
     orig_call = _lib.call
@@ -99,7 +104,9 @@ def install_timers(timer):
     _lib.call = timed_call
     ops.call = timed_call
     import nerf_pl_amd.functions as F
+    import nerf_pl_amd.optim as OP
     F.call = timed_call
+    OP.call = timed_call
 
 
 def cpu_baseline(args, budget_s):
@@ -147,31 +154,33 @@ def main():
     torch.cuda.set_device(dev)
 
     from nerf_pl_amd import Embedding, NeRF, render_rays
-    from nerf_pl_amd.rays import blender_rays
+    from nerf_pl_amd.optim import FusedAdam
+    from nerf_pl_amd.rays import RaySampler, blender_focal, pose_spherical
 
     timer = KernelTimer()
     if not args.no_kernel_timing:
         install_timers(timer)
 
-    # HBM-resident ray pool (datasets/blender.py: all rays of all train images)
+    # camera poses + target images resident in HBM (datasets/blender.py); rays
+    # are generated per batch (near/far 1/200: datasets/blender.py:40-41)
     torch.manual_seed(1234 + rank)
-    pool = blender_rays(args.img, args.poses, near=1.0, far=200.0, device=dev).contiguous()
-    pool_rgb = torch.rand(pool.shape[0], 3, device=dev)
+    poses = torch.stack([pose_spherical(-180.0 + 360.0 * k / args.poses, -30.0, 4.0)
+                         for k in range(args.poses)]).to(dev)
+    pool_rgb = torch.rand(args.poses * args.img * args.img, 3, device=dev)
+    sampler = RaySampler(poses, args.img, args.img, blender_focal(args.img), 1.0, 200.0,
+                         rgb_pool=pool_rgb, seed=99 + rank)
     torch.manual_seed(0)                      # identical initial weights on every rank
     models = [NeRF().to(dev), NeRF().to(dev)]
     emb = [Embedding(3, 10), Embedding(3, 4)]
     params = [p for m in models for p in m.parameters()]
-    opt = torch.optim.Adam(params, lr=5e-4, eps=1e-8)
-    gen = torch.Generator(device=dev).manual_seed(99 + rank)
+    opt = FusedAdam(params, lr=5e-4, eps=1e-8)
     reducer = None
     if world > 1:
         from nerf_pl_amd.distributed import GradAllReducer
         reducer = GradAllReducer(params)
 
     def step():
-        idx = torch.randint(0, pool.shape[0], (args.batch,), device=dev, generator=gen)
-        rays = pool.index_select(0, idx)
-        rgbs = pool_rgb.index_select(0, idx)
+        rays, rgbs = sampler.next(args.batch)
         res = render_rays(models, emb, rays, args.n_samples, False, 1.0, 1.0,
                           args.n_importance, 32768, False)
         loss = torch.mean((res["rgb_coarse"] - rgbs) ** 2) + torch.mean((res["rgb_fine"] - rgbs) ** 2)
@@ -246,8 +255,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (Blender-lego 400x400 camera orbit rays, random targets, "
-                    "seeded default-init NeRF coarse+fine)",
+            "data": "synthetic (Blender-lego 400x400, 100-pose camera orbit, rays generated "
+                    "on device per batch, random target colours, seeded default-init NeRF "
+                    "coarse+fine)",
             "config": {"workload": "cfg2: Blender lego 400x400, 64 coarse + 128 fine, "
                                    f"batch {args.batch} rays/rank, perturb=1, noise_std=1, "
                                    "MSE coarse+fine, Adam lr 5e-4",

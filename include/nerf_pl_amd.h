@@ -113,6 +113,32 @@ int nr_sample_pdf(const float* weights, int n_samples, const float* rays,
                   const float* z_coarse, const float* u, const float* jitter, uint64_t seed,
                   int64_t n_rays, int n_importance, float* z_pdf, float* z_fine, void* stream);
 
+/* Training-batch ray generation (datasets/ray_utils.py:5-93 get_ray_directions
+ * + get_rays [+ get_ndc_rays], the ray buffers of datasets/blender.py:54-86 and
+ * llff.py:213-249): ray k is global pixel g = sel[k] (or k when sel == NULL) =
+ * pose*H*W + row*W + col of the poses c2w (n_poses,3,4).  Direction
+ * ((col - w_half)/focal, -(row - h_half)/focal, -1) rotated by c2w and
+ * normalised, origin c2w[:,3]; rays (n,8) = [o, d, near, far].  ndc != 0 applies
+ * get_ndc_rays with near plane ndc_near and the host-evaluated constants
+ * ndc_cw = -1/(W/(2 focal)), ndc_ch = -1/(H/(2 focal)), ndc_2near = 2 ndc_near.
+ * rgb_pool (n_poses*H*W, 3) / rgb_out (n,3): optional target gather.  An
+ * out-of-range sel entry yields a NaN ray. */
+int nr_gen_rays(const float* c2w, int64_t n_poses, int H, int W, float w_half, float h_half,
+                float focal, float near, float far, int ndc, float ndc_near, float ndc_cw,
+                float ndc_ch, float ndc_2near, const int64_t* sel, int64_t n,
+                const float* rgb_pool, float* rgb_out, float* rays, void* stream);
+
+/* Fused Adam step (torch.optim.Adam as built by utils/__init__.py:10-30, the
+ * single-tensor formulas op for op) over `count` <= nr_adam_max_tensors()
+ * tensors in one launch: tables of device pointers (host arrays) to params,
+ * grads (an entry may be NULL: zero gradient), exp_avg, exp_avg_sq and their
+ * element counts.  step = the step number after increment (1 on the first). */
+int nr_adam_max_tensors(void);
+int nr_adam_step(float* const* params, const float* const* grads, float* const* exp_avg,
+                 float* const* exp_avg_sq, const int64_t* numel, int count, double lr,
+                 double beta1, double beta2, double eps, double weight_decay, int64_t step,
+                 void* stream);
+
 /* ---- shadow mapping (config 5: train_efficient_sm.py) ---------------------
  * get_normed_w column 3 (efficient_shadow_mapping.py:41-58): out (n) =
  * depth / (|camera @ pixel| + 1e-5); camera (3,3) row-major, pixels (n,3). */

@@ -30,6 +30,11 @@ SIGNATURES = {
                          _p, _p],
     "nr_composite_bwd": [_p, _i, _i, _p, _p, _p, _f, _u64, _i, _i64, _i, _i, _p, _p, _p, _p,
                          _p],
+    "nr_gen_rays": [_p, _i64, _i, _i, _f, _f, _f, _f, _f, _i, _f, _f, _f, _f, _p, _i64, _p, _p,
+                    _p, _p],
+    "nr_adam_max_tensors": [],
+    "nr_adam_step": [_p, _p, _p, _p, _p, _i, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                     ctypes.c_double, ctypes.c_double, _i64, _p],
     "nr_sm_normed_depth": [_p, _p, _p, _i64, _p, _p],
     "nr_sm_forward": [_p, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _f, _f, _i, _f, _i64, _p, _p,
                       _p],
@@ -41,7 +46,7 @@ SIGNATURES = {
     "nr_layout_query": [_i],
     "nr_last_error": [],
 }
-_RESTYPES = {"nr_layout_query": _i64, "nr_wgrad_workspace_bytes": _i64,
+_RESTYPES = {"nr_layout_query": _i64, "nr_adam_max_tensors": _i, "nr_wgrad_workspace_bytes": _i64,
              "nr_sm_workspace_bytes": _i64, "nr_last_error": ctypes.c_char_p}
 
 _lib = None

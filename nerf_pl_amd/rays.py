@@ -106,3 +106,65 @@ def llff_ndc_rays(img_w: int = 504, img_h: int = 378, n_poses: int = 4,
         nf = torch.tensor([0.0, 1.0], dtype=torch.float32, device=device).expand(o.shape[0], 2)
         out.append(torch.cat([o_ndc, d_ndc, nf], 1))
     return torch.cat(out, 0)
+
+
+def generate_rays(c2w: torch.Tensor, H: int, W: int, focal: float, near: float, far: float,
+                  sel: torch.Tensor = None, ndc: bool = False, ndc_near: float = 1.0,
+                  rgb_pool: torch.Tensor = None):
+    """Rays (n, 8) for global pixel indices ``sel`` (pose*H*W + row*W + col) of
+    the poses ``c2w`` (n_poses, 3, 4), generated on the device by
+    ``nr_gen_rays`` -- the batch the reference assembles from its precomputed
+    ray buffer (datasets/blender.py:54-86, llff.py:213-249).  ``sel=None``
+    means every pixel of every pose.  With ``rgb_pool`` (n_poses*H*W, 3) the
+    target colours of the same pixels are returned too.  With ``ndc`` the
+    forward-facing transform (get_ndc_rays, near plane ``ndc_near``) is applied
+    and near/far become 0/1 (llff.py:236-242)."""
+    from . import ops
+    from ._lib import call, ptr, stream_of
+    c2w = ops._dev(c2w.to(torch.float32), "c2w")
+    if c2w.shape[-2:] != (3, 4):
+        raise ValueError(f"c2w must be (n_poses, 3, 4), got {tuple(c2w.shape)}")
+    dev = c2w.device
+    n_poses = c2w.reshape(-1, 12).shape[0]
+    if sel is not None:
+        sel = sel.to(device=dev, dtype=torch.int64).contiguous()
+        n = sel.shape[0]
+    else:
+        n = n_poses * H * W
+    rays = torch.empty(n, 8, device=dev)
+    rgb_out = None
+    if rgb_pool is not None:
+        rgb_pool = ops._dev(rgb_pool, "rgb_pool", 3)
+        rgb_out = torch.empty(n, 3, device=dev)
+    if ndc:
+        near, far = 0.0, 1.0
+    call("nr_gen_rays", ptr(c2w), n_poses, H, W, float(W / 2), float(H / 2), float(focal),
+         float(near), float(far), int(ndc), float(ndc_near), -1. / (W / (2. * focal)),
+         -1. / (H / (2. * focal)), 2. * ndc_near, ptr(sel), n, ptr(rgb_pool), ptr(rgb_out),
+         ptr(rays), stream_of(dev))
+    return (rays, rgb_out) if rgb_pool is not None else rays
+
+
+class RaySampler:
+    """Shuffled training batches generated on the device -- replaces the
+    reference's ray buffer + ``DataLoader(shuffle=True, batch_size=B)``
+    (train.py:89-94): each epoch is a random permutation of all pixels of all
+    poses (torch.randperm on the device), each batch is produced by one
+    ``nr_gen_rays`` launch that also gathers the target colours."""
+
+    def __init__(self, c2w, H, W, focal, near, far, rgb_pool=None, ndc=False, seed=0):
+        self.c2w = c2w
+        self.H, self.W, self.focal, self.near, self.far = H, W, focal, near, far
+        self.rgb_pool, self.ndc = rgb_pool, ndc
+        self.total = c2w.reshape(-1, 12).shape[0] * H * W
+        self.gen = torch.Generator(device=c2w.device).manual_seed(seed)
+        self.perm, self.pos = None, 0
+
+    def next(self, batch: int):
+        if self.perm is None or self.pos + batch > self.total:
+            self.perm = torch.randperm(self.total, device=self.c2w.device, generator=self.gen)
+            self.pos = 0
+        sel = self.perm[self.pos:self.pos + batch]
+        self.pos += batch
+        return generate_rays(self.c2w, self.H, self.W, self.focal, self.near, self.far, sel,
+                             self.ndc, rgb_pool=self.rgb_pool)

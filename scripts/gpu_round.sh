@@ -12,6 +12,7 @@ step() {  # step <name> <timeout-seconds> <cmd...>
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
     return 0
 }
+n=0
 for s in "$@"; do
     case $s in
         tests) step tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
@@ -20,6 +21,6 @@ for s in "$@"; do
         benchq) step benchq 300 python bench.py --steps 10 --warmup 3 --cpu-baseline-seconds 0 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-baseline-seconds 0 --no-kernel-timing ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        *) step custom 600 bash -c "$s" ;;
+        *) n=$((n+1)); step custom$n 600 bash -c "$s" ;;
     esac
 done

@@ -1,0 +1,83 @@
+"""On-device ray generation (nr_gen_rays) against the ray_utils restatement
+(oracle/rays_oracle.py).  Tolerance: 2e-6 abs on Blender rays (unit directions,
+origins copied), 1e-5 relative on NDC rays (three divisions deep)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import rays_oracle as RO
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def orbit(n):
+    from nerf_pl_amd.rays import pose_spherical
+    return torch.stack([pose_spherical(-180 + 360 * k / n, -30 + 7 * k, 4.0 + 0.1 * k)
+                        for k in range(n)])
+
+
+def test_blender_rays_match_oracle():
+    from nerf_pl_amd.rays import blender_focal, generate_rays
+    H, W = 37, 41
+    poses = orbit(3)
+    f = blender_focal(W)
+    ref = RO.ray_buffer(poses, H, W, f, 2.0, 6.0)
+    got = generate_rays(poses.to(DEV), H, W, f, 2.0, 6.0).cpu()
+    assert got.shape == ref.shape
+    assert (got - ref).abs().max().item() < 2e-6
+    assert torch.equal(got[:, :3], ref[:, :3]) and torch.equal(got[:, 6:], ref[:, 6:])
+
+
+def test_ndc_rays_match_oracle():
+    from nerf_pl_amd.rays import generate_rays
+    H, W, f = 31, 45, 40.0
+    poses = []
+    for k in range(2):
+        c2w = torch.eye(4)[:3].clone()
+        c2w[:, 3] = torch.tensor([0.1 * math.cos(k), 0.1 * math.sin(k), 0.05 * k])
+        poses.append(c2w)
+    poses = torch.stack(poses)
+    ref = RO.ray_buffer(poses, H, W, f, 0.0, 1.0, ndc=True)
+    got = generate_rays(poses.to(DEV), H, W, f, 2.0, 6.0, ndc=True).cpu()
+    rel = (got - ref).abs() / ref.abs().clamp_min(1.0)
+    assert rel.max().item() < 1e-5
+    assert torch.equal(got[:, 6:], ref[:, 6:])
+
+
+def test_selected_rays_gather_targets_and_reject_bad_indices():
+    from nerf_pl_amd.rays import generate_rays
+    H = W = 16
+    poses = orbit(4)
+    total = 4 * H * W
+    rgb = torch.arange(total * 3, dtype=torch.float32).view(total, 3)
+    g = torch.Generator().manual_seed(0)
+    sel = torch.randint(0, total, (1000,), generator=g)
+    ref = RO.ray_buffer(poses, H, W, 20.0, 1.0, 200.0)[sel]
+    rays, tgt = generate_rays(poses.to(DEV), H, W, 20.0, 1.0, 200.0, sel.to(DEV),
+                              rgb_pool=rgb.to(DEV))
+    assert (rays.cpu() - ref).abs().max().item() < 2e-6
+    assert torch.equal(tgt.cpu(), rgb[sel])
+    bad = generate_rays(poses.to(DEV), H, W, 20.0, 1.0, 200.0,
+                        torch.tensor([-1, total, 5], device=DEV)).cpu()
+    assert torch.isnan(bad[:2]).all() and not torch.isnan(bad[2]).any()
+
+
+def test_ray_sampler_epochs_are_permutations():
+    from nerf_pl_amd.rays import RaySampler
+    H = W = 8
+    poses = orbit(2)
+    total = 2 * H * W
+    rgb = torch.arange(total, dtype=torch.float32).repeat_interleave(3).view(total, 3)
+    s = RaySampler(poses.to(DEV), H, W, 10.0, 2.0, 6.0, rgb_pool=rgb.to(DEV), seed=3)
+    seen = []
+    for _ in range(total // 32):
+        rays, tgt = s.next(32)
+        assert rays.shape == (32, 8)
+        seen.append(tgt[:, 0].cpu())
+    ids = torch.cat(seen).long()
+    assert torch.equal(torch.sort(ids).values, torch.arange(total))
+    ref = RO.ray_buffer(poses, H, W, 10.0, 2.0, 6.0)[ids[-32:]]
+    assert (rays.cpu() - ref).abs().max().item() < 2e-6
