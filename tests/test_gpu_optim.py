@@ -5,7 +5,7 @@ for op, but torch's vectorised CPU kernels fuse some multiply-adds (lerp,
 add with alpha), so the two drift by ulps -- and where g + wd*p cancels, Adam's
 normalisation m / sqrt(v) turns that ulp into a visible fraction of one step.
 Tolerance: parameters within 4 ulps of max(1,|p|) plus 2% of one step (lr);
-moments within 1e-6 of the tensor's max."""
+moments within 1e-5 of the tensor's max."""
 import pytest
 import torch
 
@@ -42,7 +42,7 @@ def test_fused_adam_matches_torch(wd):
     for r, q in zip(ref, ours):
         for key in ("exp_avg", "exp_avg_sq"):
             a, b = o_our.state[q][key].cpu(), o_ref.state[r][key]
-            assert (a - b).abs().max() <= 1e-6 * b.abs().max()
+            assert (a - b).abs().max() <= 1e-5 * b.abs().max()
     st_r, st_o = o_ref.state[ref[0]], o_our.state[ours[0]]
     assert float(st_r["step"]) == float(st_o["step"]) == 6.0
     assert float(o_our.state[ours[5]]["step"]) == 3.0
