@@ -59,6 +59,23 @@ int nr_mlp_fwd(const float* packed_fwd, const float* rays, const float* z, int64
                int samples_per_ray, const float* x, int xstride, int sigma_only, float* out,
                float* save, void* stream);
 
+/* bf16x6 arithmetic (the default): every fp32 operand split exactly into three
+ * bf16 pieces, the six piece products of order <= 2^-16 accumulated in fp32 on
+ * v_mfma_f32_32x32x16_bf16 -- fp32-level accuracy at 2.67x the fp32 MFMA rate.
+ * nr_pack_x3 builds its forward weight buffer (nr_fwd3_packed_bytes() bytes:
+ * the fp32 head block, then bf16 k-groups) from the flat parameters with the
+ * maps of packing.build_fwd3_map (map: flat*4 + piece, -1 = 0; n entries);
+ * nr_mlp_fwd_x3 / nr_mlp_sigma_points_x3 have the contracts of nr_mlp_fwd /
+ * nr_mlp_sigma_points and write the same saved activations. */
+int64_t nr_fwd3_packed_bytes(void);
+int nr_pack_x3(const float* flat, const int32_t* map, int64_t n, const int32_t* head_map,
+               void* out, void* stream);
+int nr_mlp_fwd_x3(const void* packed, const float* rays, const float* z, int64_t n,
+                  int samples_per_ray, const float* x, int xstride, int sigma_only, float* out,
+                  float* save, void* stream);
+int nr_mlp_sigma_points_x3(const void* packed, const float* pts, int64_t n, float* sigma_out,
+                           void* stream);
+
 /* Dense sigma query (extract_color_mesh.py:114-137, the marching-cubes grid):
  * sigma_out (n) = NeRF sigma head at points pts (n,3) -- the sigma-only fused
  * kernel with the positional encoding computed in-kernel (sigma does not
@@ -68,8 +85,10 @@ int nr_mlp_sigma_points(const float* packed_fwd, const float* pts, int64_t n, fl
 
 /* MLP backward, data-gradient chain (autograd of nerf.py:83-124): from
  * g_out (n,4) = d[rgb, sigma] writes every layer's pre-activation gradient to
- * grad_ws (n*nr_layout_query(4) floats). */
-int nr_mlp_bwd(const float* packed_bwd, const float* packed_fwd, const float* out,
+ * grad_ws (n*nr_layout_query(4) floats).  head: the fp32 head block of the
+ * forward weights (nr_layout_query(5) floats: packed_fwd + nr_layout_query(1)
+ * floats for the fp32 layout, the start of the bf16x6 buffer). */
+int nr_mlp_bwd(const float* packed_bwd, const float* head, const float* out,
                const float* g_out, const float* save, int64_t n, float* grad_ws, void* stream);
 
 /* MLP backward, weight gradients: sum over all n samples of dz^T x for every

@@ -21,6 +21,10 @@ _f = ctypes.c_float
 SIGNATURES = {
     "nr_mlp_fwd": [_p, _p, _p, _i64, _i, _p, _i, _i, _p, _p, _p],
     "nr_mlp_sigma_points": [_p, _p, _i64, _p, _p],
+    "nr_fwd3_packed_bytes": [],
+    "nr_pack_x3": [_p, _p, _i64, _p, _p, _p],
+    "nr_mlp_fwd_x3": [_p, _p, _p, _i64, _i, _p, _i, _i, _p, _p, _p],
+    "nr_mlp_sigma_points_x3": [_p, _p, _i64, _p, _p],
     "nr_mlp_bwd": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
     "nr_sm_workspace_bytes": [_i64],
@@ -46,7 +50,7 @@ SIGNATURES = {
     "nr_layout_query": [_i],
     "nr_last_error": [],
 }
-_RESTYPES = {"nr_layout_query": _i64, "nr_adam_max_tensors": _i, "nr_wgrad_workspace_bytes": _i64,
+_RESTYPES = {"nr_layout_query": _i64, "nr_adam_max_tensors": _i, "nr_fwd3_packed_bytes": _i64, "nr_wgrad_workspace_bytes": _i64,
              "nr_sm_workspace_bytes": _i64, "nr_last_error": ctypes.c_char_p}
 
 _lib = None

@@ -30,7 +30,7 @@ __device__ __forceinline__ void relu_mask(f32x16 (&acc)[NT], uint4 m) {
 
 struct BwdArgs {
     const float* packed_bwd;
-    const float* packed_fwd;   // head block: sigma / rgb weights
+    const float* head;         // fp32 head block: sigma / rgb weights
     const float* out;          // (n,4) forward output [rgb, sigma]
     const float* g_out;        // (n,4) d[rgb, sigma]
     const float* save;
@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     const bool valid = s_raw < a.n;
     const int s = valid ? s_raw : a.n - 1;
     const float* PB = a.packed_bwd;
-    const float* H = a.packed_fwd + NR_F_HEAD;
+    const float* H = a.head;
     const float* SV = a.save;
     float* const GD = a.grad;
     // The wave's 9 ReLU-mask words per lane arrive by LDS-DMA up front (one
@@ -157,17 +157,17 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
 
 }  // namespace
 
-NR_API int nr_mlp_bwd(const float* packed_bwd, const float* packed_fwd, const float* out,
+NR_API int nr_mlp_bwd(const float* packed_bwd, const float* head, const float* out,
                       const float* g_out, const float* save, int64_t n, float* grad_ws,
                       void* stream) {
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_bwd: n out of range");
     if (n == 0) return 0;
-    NR_REQUIRE(packed_bwd && packed_fwd && out && g_out && save && grad_ws,
+    NR_REQUIRE(packed_bwd && head && out && g_out && save && grad_ws,
                "nr_mlp_bwd: null pointer");
     NR_REQUIRE((((uintptr_t)out | (uintptr_t)g_out | (uintptr_t)save | (uintptr_t)grad_ws |
-                 (uintptr_t)packed_bwd | (uintptr_t)packed_fwd) & 15) == 0,
+                 (uintptr_t)packed_bwd | (uintptr_t)head) & 15) == 0,
                "nr_mlp_bwd: pointers must be 16-byte aligned");
-    BwdArgs a{packed_bwd, packed_fwd, out, g_out, save, (int)n, grad_ws};
+    BwdArgs a{packed_bwd, head, out, g_out, save, (int)n, grad_ws};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
     mlp_bwd_kernel<<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
     NR_LAUNCH_CHECK("nr_mlp_bwd");

@@ -7,6 +7,7 @@ raise.
 from __future__ import annotations
 
 import functools
+import os
 
 import numpy as np
 import torch
@@ -15,6 +16,12 @@ from . import packing
 from ._lib import call, lib, ptr, stream_of
 
 BLK = 32                                                # samples per block (one wave)
+# MLP arithmetic: "bf16x6" (fp32 operands split into three bf16 pieces on
+# v_mfma_f32_32x32x16_bf16, fp32-level accuracy, 2.67x the fp32 MFMA rate) or
+# "fp32" (v_mfma_f32_32x32x2_f32).  Both are fp32-accurate; see DESIGN.md.
+MATH = os.environ.get("NERF_PL_AMD_MATH", "bf16x6")
+if MATH not in ("bf16x6", "fp32"):
+    raise ValueError(f"NERF_PL_AMD_MATH must be 'bf16x6' or 'fp32', got {MATH!r}")
 # csrc/layout.h NR_SAVE_PER_BLOCK / NR_GRAD_PER_BLOCK (block-native layout)
 SAVE_PER_BLOCK = BLK * (64 + 8 * 256 + 256 + 128 + 32) + 9 * 256
 GRAD_PER_BLOCK = BLK * (9 * 256 + 128 + 4)
@@ -55,7 +62,40 @@ def linspace_table(n: int, device_index: int) -> torch.Tensor:
     return torch.linspace(0, 1, n).to(torch.device("cuda", device_index))
 
 
-def pack_fwd(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+@functools.lru_cache(maxsize=None)
+def _maps3(device_index: int):
+    dev = torch.device("cuda", device_index)
+    m, h = packing.build_fwd3_map()
+    return torch.from_numpy(m).to(dev), torch.from_numpy(h).to(dev)
+
+
+FWD3_BYTES = packing.fwd3_offsets()[1]
+
+
+def pack_fwd(flat: torch.Tensor, out: torch.Tensor | None = None, math: str | None = None):
+    """Forward weights in the layout of the active MLP arithmetic (``MATH``):
+    float32 fragment order, or the bf16x6 byte buffer (uint8 tensor)."""
+    if (math or MATH) == "bf16x6":
+        return pack_fwd3(flat, out)
+    return pack_fwd_fp32(flat, out)
+
+
+def pack_fwd3(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    m, hm = _maps3(flat.device.index)
+    out = torch.empty(FWD3_BYTES, dtype=torch.uint8, device=flat.device) if out is None else out
+    call("nr_pack_x3", ptr(flat), ptr(m), m.numel(), ptr(hm), ptr(out), stream_of(flat.device))
+    return out
+
+
+def head_ptr(packed: torch.Tensor) -> int:
+    """Address of the fp32 head block (biases, sigma/rgb heads) of a forward
+    packed buffer of either layout."""
+    if packed.dtype == torch.uint8:
+        return packed.data_ptr()
+    return packed.data_ptr() + 4 * packing.layer_offsets(packing.FWD_LAYERS)[1]
+
+
+def pack_fwd_fp32(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     m, _ = _maps(flat.device.index)
     out = torch.empty(FWD_PACKED, device=flat.device) if out is None else out
     call("nr_pack", ptr(flat), ptr(m), m.numel(), ptr(out), stream_of(flat.device))
@@ -83,7 +123,8 @@ def mlp_forward(packed: torch.Tensor, *, rays=None, z=None, samples_per_ray=0, x
     dev = packed.device
     out = torch.empty(n, 1 if sigma_only else 4, device=dev)
     sv = torch.empty(n_blocks(n) * SAVE_PER_BLOCK, device=dev) if save else None
-    call("nr_mlp_fwd", ptr(packed), ptr(rays), ptr(z), n, int(samples_per_ray), ptr(x), xstride,
+    entry = "nr_mlp_fwd_x3" if packed.dtype == torch.uint8 else "nr_mlp_fwd"
+    call(entry, ptr(packed), ptr(rays), ptr(z), n, int(samples_per_ray), ptr(x), xstride,
          int(sigma_only), ptr(out), ptr(sv), stream_of(dev))
     return out, sv
 
@@ -92,8 +133,8 @@ def sigma_points(packed, pts):
     """sigma (n,) of the fused sigma-only MLP at points (n,3)."""
     pts = _dev(pts, "pts", 3)
     out = torch.empty(pts.shape[0], device=pts.device)
-    call("nr_mlp_sigma_points", ptr(packed), ptr(pts), pts.shape[0], ptr(out),
-         stream_of(pts.device))
+    entry = "nr_mlp_sigma_points_x3" if packed.dtype == torch.uint8 else "nr_mlp_sigma_points"
+    call(entry, ptr(packed), ptr(pts), pts.shape[0], ptr(out), stream_of(pts.device))
     return out
 
 

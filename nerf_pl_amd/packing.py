@@ -216,3 +216,86 @@ def build_bwd_map():
     m = np.concatenate(parts).astype(np.int32)
     assert m.size == layer_offsets(BWD_LAYERS)[1]
     return m
+
+
+# -- bf16x6 split-operand layout (v_mfma_f32_32x32x16_bf16) --------------------
+# Each fp32 operand is split exactly into three bf16 pieces x = hi + mid + lo
+# (round-to-nearest at each step) and a product is formed from the six piece
+# products whose order is at most 2^-16 (hi*hi, hi*mid, mid*hi, hi*lo, lo*hi,
+# mid*mid), accumulated in fp32: fp32-level accuracy (the dropped terms are
+# <= 2^-25 relative) at 16/6 = 2.67x the fp32 MFMA rate.
+#
+# One k-group = 16 input features.  A 256-wide accumulator input supplies
+# k-group G from tile G>>1, registers 8(G&1)..8(G&1)+7: element j of lane half h
+# is feature kmap3(G, h, j) = 32(G>>1) + 16(G&1) + 8(j>>2) + 4h + (j&3).
+# Positional encodings keep the per-lane k-step order of the fp32 path:
+# element j of k-group G is the lane's pe[8G + j].
+#
+# Packed group: [piece 3][tile NT][lane 64][j 8] bf16 = NT * 3 KiB, so one
+# ds_read_b128 / global_load_lds_dwordx4 moves one (piece, tile) fragment.
+# Buffer: [head fp32, HEAD_SIZE floats][groups of every layer, in order].
+def kmap3(G, h, j):
+    G, h, j = np.asarray(G), np.asarray(h), np.asarray(j)
+    return 32 * (G >> 1) + 16 * (G & 1) + 8 * (j >> 2) + 4 * h + (j & 3)
+
+
+FWD3_LAYERS = OrderedDict([          # name -> (k-groups, tiles)
+    ("L1", (4, 8)),
+    ("L2", (16, 8)), ("L3", (16, 8)), ("L4", (16, 8)),
+    ("L5", (20, 8)),
+    ("L6", (16, 8)), ("L7", (16, 8)), ("L8", (16, 8)),
+    ("final", (16, 8)),
+    ("dir", (18, 4)),
+])
+HEAD_BYTES = HEAD_SIZE * 4
+
+
+def fwd3_offsets():
+    """Byte offset of every layer's first group, and the total buffer size."""
+    offs, o = OrderedDict(), HEAD_BYTES
+    for k, (ng, nt) in FWD3_LAYERS.items():
+        offs[k] = o
+        o += ng * nt * 3 * 1024
+    return offs, o
+
+
+def _fwd3_layer_map(w_name, segs, ntiles, offs):
+    """int32 per bf16 slot: flat_index * 4 + piece, or -1 (zero)."""
+    w_off, (rows, fan) = offs[w_name]
+    parts = []
+    for ngroups, kind, col0 in segs:
+        e = np.arange(ngroups * 3 * ntiles * 512)
+        G = e // (3 * ntiles * 512)
+        rem = e % (3 * ntiles * 512)
+        piece = rem // (ntiles * 512)
+        T = (rem % (ntiles * 512)) // 512
+        lane = (rem % 512) // 8
+        j = rem % 8
+        h = lane >> 5
+        row = 32 * T + (lane & 31)
+        if kind == "acc":
+            col = kmap3(G, h, j)
+        elif kind == "pe":
+            col = PE_MAP[8 * G + j, h]
+        else:
+            col = DIR_MAP[8 * G + j, h]
+        ok = (col >= 0) & (row < rows)
+        parts.append(np.where(ok, (w_off + row * fan + col0 + np.maximum(col, 0)) * 4 + piece, -1))
+    return np.concatenate(parts)
+
+
+def build_fwd3_map():
+    """(group map over every bf16 slot, head map over HEAD_SIZE floats)."""
+    offs, _ = param_offsets()
+    L = lambda i: f"xyz_encoding_{i}.0.weight"  # noqa: E731
+    parts = [_fwd3_layer_map(L(1), [(4, "pe", 0)], 8, offs)]
+    for i in (2, 3, 4):
+        parts.append(_fwd3_layer_map(L(i), [(16, "acc", 0)], 8, offs))
+    parts.append(_fwd3_layer_map(L(5), [(4, "pe", 0), (16, "acc", XYZ_CH)], 8, offs))
+    for i in (6, 7, 8):
+        parts.append(_fwd3_layer_map(L(i), [(16, "acc", 0)], 8, offs))
+    parts.append(_fwd3_layer_map("xyz_encoding_final.weight", [(16, "acc", 0)], 8, offs))
+    parts.append(_fwd3_layer_map("dir_encoding.0.weight", [(16, "acc", 0), (2, "dir", W)], 4, offs))
+    m = np.concatenate(parts).astype(np.int32)
+    assert m.size * 2 + HEAD_BYTES == fwd3_offsets()[1]
+    return m, _head_map(offs).astype(np.int32)

@@ -1,5 +1,6 @@
 """Isolated timing of the fused MLP kernels at the cfg2 fine-pass size
-(786,432 samples), for profiling (dev tool).  Usage: kbench.py [fwd|fwdsave|bwd|wgrad|all] [reps]"""
+(786,432 samples), for profiling (dev tool).
+Usage: kbench.py [fwd|fwdsave|fwd3|fwd3save|bwd|wgrad|all] [reps]"""
 import os
 import sys
 import time
@@ -11,7 +12,9 @@ from nerf_pl_amd import ops, packing
 from nerf_pl_amd._lib import call, stream_of
 from nerf_pl_amd.functions import _wgrad_workspace
 
-FLOP = {"fwd": 1186816, "fwdsave": 1186816, "bwd": 1115392, "wgrad": 1186816}
+FLOP = {"fwd": 1186816, "fwdsave": 1186816, "fwd3": 1186816, "fwd3save": 1186816,
+        "bwd": 1115392, "wgrad": 1186816}
+PEAK3 = 2516.6 / 6     # bf16 dense MFMA peak / 6 products: fp32-equivalent ceiling of bf16x6
 
 
 def main():
@@ -20,7 +23,8 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     flat = (torch.rand(packing.N_PARAMS, device=dev) - 0.5) * 0.15
-    pf, pb = ops.pack_fwd(flat), ops.pack_bwd(flat)
+    pf, pb = ops.pack_fwd_fp32(flat), ops.pack_bwd(flat)
+    p3 = ops.pack_fwd3(flat)
     n_rays, spr = 4096, 192
     n = n_rays * spr
     rays = torch.randn(n_rays, 8, device=dev)
@@ -41,13 +45,19 @@ def main():
         elif k == "fwdsave":
             call("nr_mlp_fwd", pf.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0,
                  out.data_ptr(), sv.data_ptr(), st)
+        elif k == "fwd3":
+            call("nr_mlp_fwd_x3", p3.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0,
+                 out.data_ptr(), None, st)
+        elif k == "fwd3save":
+            call("nr_mlp_fwd_x3", p3.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0,
+                 out.data_ptr(), sv.data_ptr(), st)
         elif k == "bwd":
-            call("nr_mlp_bwd", pb.data_ptr(), pf.data_ptr(), out.data_ptr(), gout.data_ptr(),
+            call("nr_mlp_bwd", pb.data_ptr(), ops.head_ptr(pf), out.data_ptr(), gout.data_ptr(),
                  sv.data_ptr(), n, gw.data_ptr(), st)
         elif k == "wgrad":
             call("nr_wgrad", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
 
-    ks = ["fwd", "fwdsave", "bwd", "wgrad"] if which == "all" else [which]
+    ks = ["fwd", "fwdsave", "fwd3", "fwd3save", "bwd", "wgrad"] if which == "all" else [which]
     run("bwd")
     for k in ks:
         for _ in range(2):
@@ -61,8 +71,9 @@ def main():
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         tf = n * FLOP[k] / (ms * 1e-3) / 1e12
-        print(f"{k:8s} {ms:8.3f} ms  {tf:6.1f} TFLOP/s  {tf / 157.3 * 100:5.1f}% of fp32 MFMA peak",
-              flush=True)
+        extra = f"  {tf / PEAK3 * 100:5.1f}% of the bf16x6 ceiling" if "3" in k else ""
+        print(f"{k:8s} {ms:8.3f} ms  {tf:6.1f} TFLOP/s  {tf / 157.3 * 100:5.1f}% of fp32 MFMA peak"
+              + extra, flush=True)
 
 
 if __name__ == "__main__":

@@ -58,13 +58,42 @@ def test_pack_roundtrip():
     p = O.make_params(5)
     flat = flat_params(p)
     fm, bm = packing.build_fwd_map(), packing.build_bwd_map()
-    for packed, m in ((ops.pack_fwd(flat), fm), (ops.pack_bwd(flat), bm)):
+    for packed, m in ((ops.pack_fwd_fp32(flat), fm), (ops.pack_bwd(flat), bm)):
         exp = np.where(m >= 0, flat.cpu().numpy()[np.maximum(m, 0)], 0)
         np.testing.assert_array_equal(packed.cpu().numpy(), exp)
 
 
+def test_pack_x3_pieces():
+    """bf16x6 buffer: fp32 head block, then for every weight its three bf16
+    pieces hi = bf16(w), mid = bf16(w - hi), lo = bf16(w - hi - mid)."""
+    from nerf_pl_amd import ops, packing
+    p = O.make_params(6)
+    flat = flat_params(p)
+    buf = ops.pack_fwd3(flat).cpu()
+    m, hm = packing.build_fwd3_map()
+    head = buf[:packing.HEAD_BYTES].view(torch.float32).numpy()
+    fl = flat.cpu().numpy()
+    np.testing.assert_array_equal(head, np.where(hm >= 0, fl[np.maximum(hm, 0)], 0))
+    pieces = buf[packing.HEAD_BYTES:].view(torch.bfloat16).float().numpy()
+    assert pieces.size == m.size
+    w = torch.from_numpy(fl)
+    hi = w.to(torch.bfloat16).float()
+    mid = (w - hi).to(torch.bfloat16).float()
+    lo = (w - hi - mid).to(torch.bfloat16).float()
+    ref = torch.stack([hi, mid, lo], 1).numpy()
+    ok = m >= 0
+    np.testing.assert_array_equal(pieces[ok], ref[m[ok] >> 2, m[ok] & 3])
+    assert np.all(pieces[~ok] == 0)
+    recon = ref.astype(np.float64).sum(1)
+    assert np.all(np.abs(recon - fl) <= 2.0 ** -24 * np.abs(fl))
+
+
+MATHS = ["fp32", "bf16x6"]
+
+
+@pytest.mark.parametrize("math", MATHS)
 @pytest.mark.parametrize("case", ["cfg2_n26", "cfg2_n1200", "cfg3_ndc", "ragged", "cfg1_s32"])
-def test_mlp_forward_rays_path(case):
+def test_mlp_forward_rays_path(case, math):
     from nerf_pl_amd import ops
     fx, cfg, params, cap = oracle_case(case)
     rays = torch.from_numpy(fx["rays"]).to(DEV)
@@ -72,7 +101,7 @@ def test_mlp_forward_rays_path(case):
                       (cap.get("z_fine"), cap.get("raw_fine"), params[1])):
         if z is None:
             continue
-        packed = ops.pack_fwd(flat_params(p))
+        packed = ops.pack_fwd(flat_params(p), math=math)
         out, _ = ops.mlp_forward(packed, rays=rays, z=z.contiguous().to(DEV),
                                  samples_per_ray=z.shape[1])
         err = (out.cpu() - raw).abs().max().item()
@@ -81,7 +110,8 @@ def test_mlp_forward_rays_path(case):
         assert err < 1e-4, f"{case}: max |mlp - oracle| = {err}"
 
 
-def test_mlp_forward_embedded_and_sigma_only():
+@pytest.mark.parametrize("math", MATHS)
+def test_mlp_forward_embedded_and_sigma_only(math):
     from nerf_pl_amd import ops
     p = O.make_params(3, sigma_bias=0.3)
     g = torch.Generator().manual_seed(1)
@@ -89,7 +119,7 @@ def test_mlp_forward_embedded_and_sigma_only():
     d = torch.nn.functional.normalize(torch.randn(777, 3, generator=g), dim=-1)
     x = torch.cat([O.embed(pts, 10), O.embed(d, 4)], 1)
     ref = O.nerf_forward(p, x)
-    packed = ops.pack_fwd(flat_params(p))
+    packed = ops.pack_fwd(flat_params(p), math=math)
     out, _ = ops.mlp_forward(packed, x=x.to(DEV))
     assert (out.cpu() - ref).abs().max().item() < 2e-5
     ref_s = O.nerf_forward(p, x[:, :63].contiguous(), sigma_only=True)
@@ -98,7 +128,8 @@ def test_mlp_forward_embedded_and_sigma_only():
     assert (out_s.cpu() - ref_s).abs().max().item() < 2e-5
 
 
-def test_mlp_forward_saved_activations():
+@pytest.mark.parametrize("math", MATHS)
+def test_mlp_forward_saved_activations(math):
     """The training save buffer holds exactly the reference's intermediates."""
     from nerf_pl_amd import ops, packing
     p = O.make_params(4, sigma_bias=0.2)
@@ -108,7 +139,7 @@ def test_mlp_forward_saved_activations():
     d = torch.nn.functional.normalize(torch.randn(n, 3, generator=g), dim=-1)
     e_xyz, e_dir = O.embed(pts, 10), O.embed(d, 4)
     x = torch.cat([e_xyz, e_dir], 1)
-    packed = ops.pack_fwd(flat_params(p))
+    packed = ops.pack_fwd(flat_params(p), math=math)
     _, sv = ops.mlp_forward(packed, x=x.to(DEV), save=True)
     sv = sv.cpu()
     # oracle intermediates
