@@ -75,6 +75,12 @@ int nr_mlp_fwd_x3(const void* packed, const float* rays, const float* z, int64_t
                   float* save, void* stream);
 int nr_mlp_sigma_points_x3(const void* packed, const float* pts, int64_t n, float* sigma_out,
                            void* stream);
+/* bf16x6 data-gradient chain: nr_pack_bwd_x3 packs the transposed weights
+ * (packing.build_bwd3_map, n entries, 3,342,336 bytes); nr_mlp_bwd_x3 has the
+ * contract of nr_mlp_bwd. */
+int nr_pack_bwd_x3(const float* flat, const int32_t* map, int64_t n, void* out, void* stream);
+int nr_mlp_bwd_x3(const void* packed_bwd, const float* head, const float* out, const float* g_out,
+                  const float* save, int64_t n, float* grad_ws, void* stream);
 
 /* Dense sigma query (extract_color_mesh.py:114-137, the marching-cubes grid):
  * sigma_out (n) = NeRF sigma head at points pts (n,3) -- the sigma-only fused

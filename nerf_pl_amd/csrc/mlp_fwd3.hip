@@ -15,139 +15,28 @@
 // output tiles x 3 pieces = 24 KiB), filled by LDS-DMA (global_load_lds
 // dwordx4) kSlots-1 groups ahead; one barrier per group hands a slot over.
 // The B-fragment split costs ~45 VALU ops per k-group, hidden between MFMAs.
-#include "layout.h"
+#include "x3.h"
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+using namespace x3;
 
-constexpr int kWaves = 4;
-constexpr int kSlots = 4;                      // ring depth in k-groups
-constexpr int kSlotBytes = 3 * 8 * 1024;       // 3 pieces x 8 tiles x 1 KiB
 constexpr int kHeadBytes = NR_H_SIZE * 4;
-constexpr int kLdsBytes = kSlots * kSlotBytes + kHeadBytes;
+constexpr int kLdsBytes = kRingBytes + kHeadBytes;
 
 // ---- the k-group sequence (packing.py FWD3_LAYERS) --------------------------
-// layer: first group, groups, tiles
 constexpr int kL1 = 0, kL2 = 4, kL3 = 20, kL4 = 36, kL5 = 52, kL6 = 72, kL7 = 88, kL8 = 104;
 constexpr int kFinal = 120, kDir = 136, kQAll = 154, kQSigma = 120;
 
-__host__ __device__ constexpr int grp_tiles(int q) { return q >= kDir ? 4 : 8; }
-// byte offset of group q inside the packed buffer (head first)
-__host__ __device__ constexpr int64_t grp_off(int q) {
-    return (int64_t)kHeadBytes +
-           (q <= kDir ? (int64_t)q * 8 * 3072 : (int64_t)kDir * 8 * 3072 + (int64_t)(q - kDir) * 4 * 3072);
-}
-static_assert(grp_off(kQAll) == 3575840, "packed size must match packing.fwd3_offsets()");
-
-// DMA instructions this wave issues for group q (each moves one 1 KiB fragment)
-__host__ __device__ constexpr int grp_dma(int q) { return grp_tiles(q) * 3 / kWaves; }
-
-// vm operations this wave issued after its DMA for group q, at the time group
-// q is consumed: the DMA of the kSlots-2 groups after it (stores only add)
-template <int Q, int QEND>
-__host__ __device__ constexpr int wait_count() {
-    int n = 0;
-    for (int k = Q + 1; k <= Q + kSlots - 2; ++k)
-        if (k < QEND) n += grp_dma(k);
-    return n;
-}
-
-__device__ __forceinline__ char* slot_ptr(char* smem, int q) { return smem + (q % kSlots) * kSlotBytes; }
-
-template <int Q, int QEND>
-__device__ __forceinline__ void stage(const char* __restrict__ packed, char* smem, int wave,
-                                      int lane) {
-    if constexpr (Q < QEND) {
-        constexpr int NT = grp_tiles(Q);
-        const char* src = packed + grp_off(Q);
-        char* dst = slot_ptr(smem, Q);
-#pragma unroll
-        for (int k = 0; k < NT * 3 / kWaves; ++k) {
-            const int i = wave + kWaves * k;
-            __builtin_amdgcn_global_load_lds(
-                (const void*)(src + i * 1024 + lane * 16),
-                (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
-        }
+struct FwdTab {
+    __host__ __device__ static constexpr int tiles(int q) { return q >= kDir ? 4 : 8; }
+    // byte offset of group q inside the packed buffer (head first)
+    __host__ __device__ static constexpr int64_t off(int q) {
+        return (int64_t)kHeadBytes + (q <= kDir ? (int64_t)q * 8 * 3072
+                                                : (int64_t)kDir * 8 * 3072 + (int64_t)(q - kDir) * 4 * 3072);
     }
-}
-
-// group Q may be read once this wave's DMA landed and every wave passed here
-template <int Q, int QEND>
-__device__ __forceinline__ void ring_enter() {
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(wait_count<Q, QEND>()) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-
-// exact 3-way split of 8 fp32 values into bf16 pieces
-struct Pieces { bf16x8 hi, mid, lo; };
-__device__ __forceinline__ Pieces split8(const float (&x)[8]) {
-    Pieces p;
-#pragma unroll
-    for (int i = 0; i < 8; i += 2) {
-        const f32x2 v = {x[i], x[i + 1]};
-        const bf16x2 h = __builtin_convertvector(v, bf16x2);
-        const f32x2 r1 = v - __builtin_convertvector(h, f32x2);
-        const bf16x2 m = __builtin_convertvector(r1, bf16x2);
-        const f32x2 r2 = r1 - __builtin_convertvector(m, f32x2);
-        const bf16x2 l = __builtin_convertvector(r2, bf16x2);
-        p.hi[i] = h[0]; p.hi[i + 1] = h[1];
-        p.mid[i] = m[0]; p.mid[i + 1] = m[1];
-        p.lo[i] = l[0]; p.lo[i + 1] = l[1];
-    }
-    return p;
-}
-
-__device__ __forceinline__ f32x16 mfma_x6(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
-                                          const Pieces& b, f32x16 acc) {
-    // small terms first
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b.hi, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b.lo, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b.mid, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b.hi, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b.mid, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b.hi, acc, 0, 0, 0);
-    return acc;
-}
-
-// one k-group: acc[t] += W_q[t] * B for the NT output tiles
-template <int Q, int QEND, int NT>
-__device__ __forceinline__ void group_mm(const char* __restrict__ packed, char* smem, int wave,
-                                         int lane, f32x16 (&acc)[8], const Pieces& b) {
-    const char* s = slot_ptr(smem, Q) + lane * 16;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(s + (0 * NT + t) * 1024);
-        const bf16x8 am = *reinterpret_cast<const bf16x8*>(s + (1 * NT + t) * 1024);
-        const bf16x8 al = *reinterpret_cast<const bf16x8*>(s + (2 * NT + t) * 1024);
-        acc[t] = mfma_x6(ah, am, al, b, acc[t]);
-    }
-}
-
-template <int V> using IC = std::integral_constant<int, V>;
-
-// A layer segment of NG k-groups starting at global group Q0 (compile-time
-// recursion so that ring slots, DMA sources and wait counts are constants).
-//   getb(IC<g>, float (&x)[8]): the 8 fp32 B values of local group g
-//   side(IC<g>): saved-activation stores spread over the groups
-template <int Q0, int G, int NG, int NT, int QEND, typename GetB, typename Side>
-__device__ __forceinline__ void segment(const char* __restrict__ packed, char* smem, int wave,
-                                        int lane, f32x16 (&acc)[8], GetB& getb, Side& side) {
-    if constexpr (G < NG) {
-        constexpr int Q = Q0 + G;
-        ring_enter<Q, QEND>();
-        stage<Q + kSlots - 1, QEND>(packed, smem, wave, lane);
-        side(IC<G>());
-        float x[8];
-        getb(IC<G>(), x);
-        const Pieces b = split8(x);
-        group_mm<Q, QEND, NT>(packed, smem, wave, lane, acc, b);
-        segment<Q0, G + 1, NG, NT, QEND>(packed, smem, wave, lane, acc, getb, side);
-    }
-}
+};
+static_assert(FwdTab::off(kQAll) == 3575840, "packed size must match packing.fwd3_offsets()");
 
 template <int NT>
 __device__ __forceinline__ void init_bias(f32x16 (&acc)[8], const float* __restrict__ b, int h) {
@@ -231,10 +120,6 @@ struct Fwd3Args {
     float* out; float* save;
 };
 
-struct NoSide {
-    template <typename T> __device__ __forceinline__ void operator()(T) const {}
-};
-
 template <int MODE, bool SIGMA_ONLY>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     constexpr bool EMB = MODE == FWD_EMB;
@@ -250,16 +135,13 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     const char* P = a.packed;
 
     // head block (biases, sigma/rgb heads) -> LDS, then start the weight ring
-    float* Hs = reinterpret_cast<float*>(smem + kSlots * kSlotBytes);
+    float* Hs = reinterpret_cast<float*>(smem + kRingBytes);
     {
         const f32x4* src = reinterpret_cast<const f32x4*>(P);
         for (int i = threadIdx.x; i < NR_H_SIZE / 4; i += 64 * kWaves)
             reinterpret_cast<f32x4*>(Hs)[i] = src[i];
     }
-    stage<0, QEND>(P, smem, wave, lane);
-    stage<1, QEND>(P, smem, wave, lane);
-    stage<2, QEND>(P, smem, wave, lane);
-    static_assert(kSlots == 4, "prologue stages kSlots-1 groups");
+    prologue<FwdTab, QEND>(P, smem, wave, lane);
     __syncthreads();   // head visible (the DMA stays in flight: waited per group)
     const float* H = Hs;
     const int nb = (a.n + 31) / 32;
@@ -301,11 +183,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         };
     };
     auto from_acc = [](const f32x16 (&X)[8]) {
-        return [&X](auto gc, float (&x)[8]) {
-            constexpr int g = decltype(gc)::value;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = X[g >> 1][8 * (g & 1) + j];
-        };
+        return [&X](auto gc, float (&x)[8]) { acc_group<decltype(gc)::value>(X, x); };
     };
     NoSide none;
 
@@ -330,7 +208,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
                 *reinterpret_cast<f32x4*>(pdst + (grp * 64 + lane) * 4) = v;
             }
         };
-        segment<kL1, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, side);
+        segment<FwdTab, kL1, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, side);
         relu<8>(A);
     }
 #define NR_DENSE3(DST, SRC, Q0, L)                                              \
@@ -338,7 +216,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         init_bias<8>(DST, H + NR_H_BIAS(L), h);                                 \
         auto gb = from_acc(SRC);                                                \
         auto sd = side_acc(SRC, hseg(L - 2), mseg(L - 2));                      \
-        segment<Q0, 0, 16, 8, QEND>(P, smem, wave, lane, DST, gb, sd);          \
+        segment<FwdTab, Q0, 0, 16, 8, QEND>(P, smem, wave, lane, DST, gb, sd);          \
         relu<8>(DST);                                                           \
     }
     NR_DENSE3(B, A, kL2, 2)
@@ -354,10 +232,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = pe[8 * g + j];
         };
-        segment<kL5, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, none);
+        segment<FwdTab, kL5, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, none);
         auto gb = from_acc(B);
         auto sd = side_acc(B, hseg(3), mseg(3));
-        segment<kL5 + 4, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd);
+        segment<FwdTab, kL5 + 4, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd);
         relu<8>(A);
     }
     NR_DENSE3(B, A, kL6, 6)
@@ -374,7 +252,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             init_bias<8>(A, H + NR_H_BFINAL, h);
             auto gb = from_acc(B);
             auto sd = side_acc(B, hseg(7), mseg(7));
-            segment<kFinal, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd);
+            segment<FwdTab, kFinal, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd);
         }
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
         float dpe[NR_DIR_KSTEPS];
@@ -386,7 +264,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             float* fdst = SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256);
             auto gb = from_acc(A);
             auto sd = side_acc(A, fdst, nullptr);
-            segment<kDir, 0, 16, 4, QEND>(P, smem, wave, lane, C, gb, sd);
+            segment<FwdTab, kDir, 0, 16, 4, QEND>(P, smem, wave, lane, C, gb, sd);
         }
         {
             float* ddst = SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32);
@@ -405,7 +283,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
                     *reinterpret_cast<f32x4*>(ddst + (grp * 64 + lane) * 4) = v;
                 }
             };
-            segment<kDir + 16, 0, 2, 4, QEND>(P, smem, wave, lane, C, getb, side);
+            segment<FwdTab, kDir + 16, 0, 2, 4, QEND>(P, smem, wave, lane, C, getb, side);
         }
         relu<4>(C);
         float rgb[3];
@@ -452,12 +330,12 @@ __global__ void pack3_kernel(const float* __restrict__ flat, const int32_t* __re
 
 }  // namespace
 
-NR_API int64_t nr_fwd3_packed_bytes(void) { return grp_off(kQAll); }
+NR_API int64_t nr_fwd3_packed_bytes(void) { return FwdTab::off(kQAll); }
 
 NR_API int nr_pack_x3(const float* flat, const int32_t* map, int64_t n, const int32_t* head_map,
                       void* out, void* stream) {
-    NR_REQUIRE(n == (grp_off(kQAll) - kHeadBytes) / 2, "nr_pack_x3: map has %lld entries, "
-               "expected %lld", (long long)n, (long long)((grp_off(kQAll) - kHeadBytes) / 2));
+    NR_REQUIRE(n == (FwdTab::off(kQAll) - kHeadBytes) / 2, "nr_pack_x3: map has %lld entries, "
+               "expected %lld", (long long)n, (long long)((FwdTab::off(kQAll) - kHeadBytes) / 2));
     NR_REQUIRE(flat && map && head_map && out, "nr_pack_x3: null pointer");
     pack3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
         flat, map, n, head_map, reinterpret_cast<char*>(out));

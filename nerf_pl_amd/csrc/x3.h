@@ -1,0 +1,153 @@
+// bf16x6 split-operand MFMA machinery shared by the fused MLP kernels
+// (mlp_fwd3.hip, mlp_bwd3.hip): the exact three-piece bf16 split, the
+// six-product v_mfma_f32_32x32x16_bf16 step, and the LDS ring of weight
+// k-groups filled by LDS-DMA and handed over with one barrier per group.
+//
+// A weight table TAB describes the k-group sequence of one packed buffer:
+//   TAB::tiles(q)  output tiles (32 rows) of group q (8 or 4)
+//   TAB::off(q)    byte offset of group q; a group is [piece 3][tile][lane 64][8] bf16
+#pragma once
+#include <utility>
+#include "layout.h"
+
+namespace x3 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kWaves = 4;
+constexpr int kSlots = 4;                      // ring depth in k-groups
+constexpr int kSlotBytes = 3 * 8 * 1024;       // 3 pieces x 8 tiles x 1 KiB
+constexpr int kRingBytes = kSlots * kSlotBytes;
+
+template <int V> using IC = std::integral_constant<int, V>;
+
+// DMA instructions one wave issues for group q (each moves one 1 KiB fragment)
+template <class TAB>
+__host__ __device__ constexpr int grp_dma(int q) { return TAB::tiles(q) * 3 / kWaves; }
+
+// vm operations this wave issued after its DMA for group q by the time group
+// q is consumed: the DMA of the kSlots-2 groups after it (stores only add,
+// so the count is a safe lower bound)
+template <class TAB, int Q, int QEND>
+__host__ __device__ constexpr int wait_count() {
+    int n = 0;
+    for (int k = Q + 1; k <= Q + kSlots - 2; ++k)
+        if (k < QEND) n += grp_dma<TAB>(k);
+    return n;
+}
+
+__device__ __forceinline__ char* slot_ptr(char* ring, int q) { return ring + (q % kSlots) * kSlotBytes; }
+
+template <class TAB, int Q, int QEND>
+__device__ __forceinline__ void stage(const char* __restrict__ packed, char* ring, int wave,
+                                      int lane) {
+    if constexpr (Q < QEND) {
+        constexpr int NT = TAB::tiles(Q);
+        const char* src = packed + TAB::off(Q);
+        char* dst = slot_ptr(ring, Q);
+#pragma unroll
+        for (int k = 0; k < NT * 3 / kWaves; ++k) {
+            const int i = wave + kWaves * k;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(src + i * 1024 + lane * 16),
+                (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+        }
+    }
+}
+
+template <class TAB, int QEND>
+__device__ __forceinline__ void prologue(const char* __restrict__ packed, char* ring, int wave,
+                                         int lane) {
+    static_assert(kSlots == 4, "prologue stages kSlots-1 groups");
+    stage<TAB, 0, QEND>(packed, ring, wave, lane);
+    stage<TAB, 1, QEND>(packed, ring, wave, lane);
+    stage<TAB, 2, QEND>(packed, ring, wave, lane);
+}
+
+// group Q may be read once this wave's DMA landed and every wave passed here
+template <class TAB, int Q, int QEND>
+__device__ __forceinline__ void ring_enter() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(wait_count<TAB, Q, QEND>()) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// exact 3-way split of 8 fp32 values into bf16 pieces (round-to-nearest)
+struct Pieces { bf16x8 hi, mid, lo; };
+__device__ __forceinline__ Pieces split8(const float (&x)[8]) {
+    Pieces p;
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        const f32x2 v = {x[i], x[i + 1]};
+        const bf16x2 h = __builtin_convertvector(v, bf16x2);
+        const f32x2 r1 = v - __builtin_convertvector(h, f32x2);
+        const bf16x2 m = __builtin_convertvector(r1, bf16x2);
+        const f32x2 r2 = r1 - __builtin_convertvector(m, f32x2);
+        const bf16x2 l = __builtin_convertvector(r2, bf16x2);
+        p.hi[i] = h[0]; p.hi[i + 1] = h[1];
+        p.mid[i] = m[0]; p.mid[i + 1] = m[1];
+        p.lo[i] = l[0]; p.lo[i + 1] = l[1];
+    }
+    return p;
+}
+
+// acc += A * B with both operands given as pieces: the six products of order
+// <= 2^-16, small terms first
+__device__ __forceinline__ f32x16 mfma_x6(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
+                                          const Pieces& b, f32x16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b.hi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b.lo, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b.mid, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b.hi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b.mid, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b.hi, acc, 0, 0, 0);
+    return acc;
+}
+
+// one k-group: acc[t] += W_q[t] * B for the NT output tiles
+template <int Q, int NT>
+__device__ __forceinline__ void group_mm(char* ring, int lane, f32x16 (&acc)[8], const Pieces& b) {
+    const char* s = slot_ptr(ring, Q) + lane * 16;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(s + (0 * NT + t) * 1024);
+        const bf16x8 am = *reinterpret_cast<const bf16x8*>(s + (1 * NT + t) * 1024);
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(s + (2 * NT + t) * 1024);
+        acc[t] = mfma_x6(ah, am, al, b, acc[t]);
+    }
+}
+
+// A layer segment of NG k-groups starting at global group Q0 (compile-time
+// recursion: ring slots, DMA sources and wait counts are constants).
+//   getb(IC<g>, float (&x)[8]): the 8 fp32 B values of local group g
+//   side(IC<g>): output stores of the previous layer, spread over the groups
+template <class TAB, int Q0, int G, int NG, int NT, int QEND, typename GetB, typename Side>
+__device__ __forceinline__ void segment(const char* __restrict__ packed, char* ring, int wave,
+                                        int lane, f32x16 (&acc)[8], GetB& getb, Side& side) {
+    if constexpr (G < NG) {
+        constexpr int Q = Q0 + G;
+        ring_enter<TAB, Q, QEND>();
+        stage<TAB, Q + kSlots - 1, QEND>(packed, ring, wave, lane);
+        side(IC<G>());
+        float x[8];
+        getb(IC<G>(), x);
+        const Pieces b = split8(x);
+        group_mm<Q, NT>(ring, lane, acc, b);
+        segment<TAB, Q0, G + 1, NG, NT, QEND>(packed, ring, wave, lane, acc, getb, side);
+    }
+}
+
+// B values of k-group g of a 256-wide accumulator input (packing.kmap3)
+template <int g>
+__device__ __forceinline__ void acc_group(const f32x16 (&X)[8], float (&x)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = X[g >> 1][8 * (g & 1) + j];
+}
+
+struct NoSide {
+    template <typename T> __device__ __forceinline__ void operator()(T) const {}
+};
+
+}  // namespace x3

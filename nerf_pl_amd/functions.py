@@ -61,7 +61,8 @@ class _FusedMLP(torch.autograd.Function):
             g_out = g4
         grad_ws = torch.empty(ops.n_blocks(n) * ops.GRAD_PER_BLOCK, device=dev)
         g_out = g_out.contiguous()
-        call("nr_mlp_bwd", packed_b.data_ptr(), ops.head_ptr(packed_f), out.data_ptr(),
+        entry = "nr_mlp_bwd_x3" if packed_b.dtype == torch.uint8 else "nr_mlp_bwd"
+        call(entry, packed_b.data_ptr(), ops.head_ptr(packed_f), out.data_ptr(),
              g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), stream_of(dev))
         gflat = torch.empty(packing.N_PARAMS, device=dev)
         ws = _wgrad_workspace(dev.index)

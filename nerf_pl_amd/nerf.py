@@ -103,7 +103,7 @@ class NeRF(nn.Module):
         parameters changed (tracked through their version counters)."""
         flat = self.flat_params()
         ver = tuple(p._version for p in self.ordered_params())
-        key = (flat.data_ptr(), ver)
+        key = (flat.data_ptr(), ver, ops.MATH)
         c = self._pack_cache
         if c is None or c[0] != key:
             c = [key, ops.pack_fwd(flat), None]

@@ -102,7 +102,23 @@ def pack_fwd_fp32(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.
     return out
 
 
-def pack_bwd(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+@functools.lru_cache(maxsize=None)
+def _map_bwd3(device_index: int):
+    return torch.from_numpy(packing.build_bwd3_map()).to(torch.device("cuda", device_index))
+
+
+def pack_bwd(flat: torch.Tensor, out: torch.Tensor | None = None, math: str | None = None):
+    """Transposed weights of the data-gradient chain in the active arithmetic."""
+    if (math or MATH) == "bf16x6":
+        m = _map_bwd3(flat.device.index)
+        out = torch.empty(packing.BWD3_BYTES, dtype=torch.uint8, device=flat.device) \
+            if out is None else out
+        call("nr_pack_bwd_x3", ptr(flat), ptr(m), m.numel(), ptr(out), stream_of(flat.device))
+        return out
+    return pack_bwd_fp32(flat, out)
+
+
+def pack_bwd_fp32(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _, m = _maps(flat.device.index)
     out = torch.empty(BWD_PACKED, device=flat.device) if out is None else out
     call("nr_pack", ptr(flat), ptr(m), m.numel(), ptr(out), stream_of(flat.device))

@@ -299,3 +299,42 @@ def build_fwd3_map():
     m = np.concatenate(parts).astype(np.int32)
     assert m.size * 2 + HEAD_BYTES == fwd3_offsets()[1]
     return m, _head_map(offs).astype(np.int32)
+
+
+BWD3_LAYERS = OrderedDict([          # transposed layers of the data-gradient chain
+    ("dirT", (8, 8)), ("finalT", (16, 8)),
+    ("L8T", (16, 8)), ("L7T", (16, 8)), ("L6T", (16, 8)), ("L5T", (16, 8)),
+    ("L4T", (16, 8)), ("L3T", (16, 8)), ("L2T", (16, 8)),
+])
+BWD3_BYTES = sum(ng * nt * 3 * 1024 for ng, nt in BWD3_LAYERS.values())
+
+
+def _bwd3_layer_map(w_name, ngroups, col0, offs):
+    """Transposed layer: k runs over the forward layer's OUTPUT features
+    (kmap3 order), the 8 tiles over its input columns col0 .. col0+255."""
+    w_off, (rows, fan) = offs[w_name]
+    e = np.arange(ngroups * 3 * 8 * 512)
+    G = e // (3 * 8 * 512)
+    rem = e % (3 * 8 * 512)
+    piece = rem // (8 * 512)
+    T = (rem % (8 * 512)) // 512
+    lane = (rem % 512) // 8
+    j = rem % 8
+    k_out = kmap3(G, lane >> 5, j)
+    c_in = col0 + 32 * T + (lane & 31)
+    return (w_off + k_out * fan + c_in) * 4 + piece
+
+
+def build_bwd3_map():
+    offs, _ = param_offsets()
+    L = lambda i: f"xyz_encoding_{i}.0.weight"  # noqa: E731
+    parts = [_bwd3_layer_map("dir_encoding.0.weight", 8, 0, offs),
+             _bwd3_layer_map("xyz_encoding_final.weight", 16, 0, offs)]
+    for i in (8, 7, 6):
+        parts.append(_bwd3_layer_map(L(i), 16, 0, offs))
+    parts.append(_bwd3_layer_map(L(5), 16, XYZ_CH, offs))
+    for i in (4, 3, 2):
+        parts.append(_bwd3_layer_map(L(i), 16, 0, offs))
+    m = np.concatenate(parts).astype(np.int32)
+    assert m.size * 2 == BWD3_BYTES
+    return m

@@ -13,7 +13,7 @@ from nerf_pl_amd._lib import call, stream_of
 from nerf_pl_amd.functions import _wgrad_workspace
 
 FLOP = {"fwd": 1186816, "fwdsave": 1186816, "fwd3": 1186816, "fwd3save": 1186816,
-        "bwd": 1115392, "wgrad": 1186816}
+        "bwd": 1115392, "bwd3": 1115392, "wgrad": 1186816}
 PEAK3 = 2516.6 / 6     # bf16 dense MFMA peak / 6 products: fp32-equivalent ceiling of bf16x6
 
 
@@ -23,8 +23,8 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     flat = (torch.rand(packing.N_PARAMS, device=dev) - 0.5) * 0.15
-    pf, pb = ops.pack_fwd_fp32(flat), ops.pack_bwd(flat)
-    p3 = ops.pack_fwd3(flat)
+    pf, pb = ops.pack_fwd_fp32(flat), ops.pack_bwd_fp32(flat)
+    p3, pb3 = ops.pack_fwd3(flat), ops.pack_bwd(flat, math="bf16x6")
     n_rays, spr = 4096, 192
     n = n_rays * spr
     rays = torch.randn(n_rays, 8, device=dev)
@@ -54,10 +54,14 @@ def main():
         elif k == "bwd":
             call("nr_mlp_bwd", pb.data_ptr(), ops.head_ptr(pf), out.data_ptr(), gout.data_ptr(),
                  sv.data_ptr(), n, gw.data_ptr(), st)
+        elif k == "bwd3":
+            call("nr_mlp_bwd_x3", pb3.data_ptr(), ops.head_ptr(p3), out.data_ptr(), gout.data_ptr(),
+                 sv.data_ptr(), n, gw.data_ptr(), st)
         elif k == "wgrad":
             call("nr_wgrad", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
 
-    ks = ["fwd", "fwdsave", "fwd3", "fwd3save", "bwd", "wgrad"] if which == "all" else [which]
+    ks = ["fwd", "fwdsave", "fwd3", "fwd3save", "bwd", "bwd3", "wgrad"] if which == "all" \
+        else which.split(",")
     run("bwd")
     for k in ks:
         for _ in range(2):

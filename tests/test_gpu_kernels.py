@@ -58,7 +58,7 @@ def test_pack_roundtrip():
     p = O.make_params(5)
     flat = flat_params(p)
     fm, bm = packing.build_fwd_map(), packing.build_bwd_map()
-    for packed, m in ((ops.pack_fwd_fp32(flat), fm), (ops.pack_bwd(flat), bm)):
+    for packed, m in ((ops.pack_fwd_fp32(flat), fm), (ops.pack_bwd_fp32(flat), bm)):
         exp = np.where(m >= 0, flat.cpu().numpy()[np.maximum(m, 0)], 0)
         np.testing.assert_array_equal(packed.cpu().numpy(), exp)
 
