@@ -103,6 +103,9 @@ int nr_mlp_bwd(const float* packed_bwd, const float* head, const float* out,
 int64_t nr_wgrad_workspace_bytes(int64_t n);
 int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
              float* grad_flat, void* stream);
+/* The same weight gradients on bf16x6 split-operand MFMA (fp32-level accuracy). */
+int nr_wgrad_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                float* grad_flat, void* stream);
 
 /* Stratified coarse depths (rendering.py:216-232).  tlin = torch.linspace(0,1,S)
  * values; u: (n_rays,S) replay of torch.rand or NULL. */

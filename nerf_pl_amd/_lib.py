@@ -27,6 +27,7 @@ SIGNATURES = {
     "nr_mlp_sigma_points_x3": [_p, _p, _i64, _p, _p],
     "nr_pack_bwd_x3": [_p, _p, _i64, _p, _p],
     "nr_mlp_bwd_x3": [_p, _p, _p, _p, _p, _i64, _p, _p],
+    "nr_wgrad_x3": [_p, _p, _i64, _p, _p, _p],
     "nr_mlp_bwd": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
     "nr_sm_workspace_bytes": [_i64],

@@ -15,7 +15,7 @@
 // gradient buffer in NeRF.named_parameters() order.
 #include <stdlib.h>
 
-#include "layout.h"
+#include "x3.h"
 
 namespace {
 
@@ -255,6 +255,231 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// bf16x6 variant: the same task list and slabs on v_mfma_f32_32x32x16_bf16.
+// A stage is 16 samples (half a block): each thread loads the float4s of two
+// adjacent samples of one 4-column chunk, splits them exactly into three bf16
+// pieces (x3.h) and writes them as [piece][column][16 samples] images
+// (column stride 48 B: conflict-free ds_read_b128 fragments), double
+// buffered; the bias sums come from the fp32 values during staging.
+// ---------------------------------------------------------------------------
+namespace w3 {
+constexpr int kColB = 48;                        // bytes per column (16 bf16 + pad)
+constexpr int kPlane = 256 * kColB;              // one piece of one operand
+constexpr int kOpnd = 3 * kPlane;                // one operand (3 pieces)
+constexpr int kBufB = 2 * kOpnd;                 // one stage buffer (A + B)
+constexpr int kLds = 2 * kBufB;                  // double buffered: 147,456 B
+
+// column of element e of float4 chunk k at lane half h, and chunks per block
+template <int KIND, int W>
+struct Geo3 {
+    static constexpr int CHUNKS = KIND == SEG_ACC ? W / 8 : (KIND == SEG_PE ? 8 : (KIND == SEG_DPE ? 4 : 0));
+    __device__ static __forceinline__ int col(int k, int h) {
+        if constexpr (KIND == SEG_ACC) return 32 * (k >> 2) + 8 * (k & 3) + 4 * h;
+        else if constexpr (KIND == SEG_PE) return 32 * h + 4 * k;
+        else return 16 * h + 4 * k;
+    }
+};
+
+// one operand's half-block: loads (2 float4 per thread) and the split/store
+template <int KIND, int W>
+struct Stager {
+    bool act;      // this thread owns a pair (loads run for every thread, clamped)
+    int k, h, jp;  // chunk, lane half, sample pair
+    f32x4 v0, v1;
+    __device__ __forceinline__ void init(int tid) {
+        if constexpr (KIND == SEG_HEAD) {
+            act = tid < 8; k = 0; h = 0; jp = tid & 7;
+        } else {
+            k = tid >> 4; h = (tid >> 3) & 1; jp = tid & 7;
+            act = k < Geo3<KIND, W>::CHUNKS;
+            k = act ? k : 0;
+        }
+    }
+    // samples 16 hb + 2 jp and +1 of block blk (unconditional: keeps the
+    // compiler's vmcnt bookkeeping exact across the prefetch)
+    __device__ __forceinline__ void load(const float* base, int blk, int hb) {
+        const int j = 16 * hb + 2 * jp;
+        if constexpr (KIND == SEG_HEAD) {
+            const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * 32 + j;
+            v0 = p[0]; v1 = p[1];
+        } else {
+            constexpr int F4 = Geo3<KIND, W>::CHUNKS * 64;
+            const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * F4 + k * 64 + 32 * h + j;
+            v0 = p[0]; v1 = p[1];
+        }
+    }
+    // split + store into an operand image; samples >= nval become 0; adds the
+    // per-column sums of the two samples (bias) to s[e]
+    __device__ __forceinline__ void store(char* img, int nval, float (&s)[4]) {
+        if (!act) return;
+        const int j = 2 * jp;
+        const f32x4 a = j < nval ? v0 : f32x4{};
+        const f32x4 b = j + 1 < nval ? v1 : f32x4{};
+        const int c0 = KIND == SEG_HEAD ? 0 : Geo3<KIND, W>::col(k, h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const x3::f32x2 x = {a[e], b[e]};
+            s[e] += x[0] + x[1];
+            const x3::bf16x2 hi = __builtin_convertvector(x, x3::bf16x2);
+            const x3::f32x2 r1 = x - __builtin_convertvector(hi, x3::f32x2);
+            const x3::bf16x2 mid = __builtin_convertvector(r1, x3::bf16x2);
+            const x3::bf16x2 lo = __builtin_convertvector(r1 - __builtin_convertvector(mid, x3::f32x2),
+                                                          x3::bf16x2);
+            char* q = img + (c0 + e) * kColB + 4 * jp;
+            *reinterpret_cast<x3::bf16x2*>(q) = hi;
+            *reinterpret_cast<x3::bf16x2*>(q + kPlane) = mid;
+            *reinterpret_cast<x3::bf16x2*>(q + 2 * kPlane) = lo;
+        }
+    }
+};
+}  // namespace w3
+
+template <int KA, int WA, int KB, int WB, int WM, int WN>
+__device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, int b0, int b1,
+                                            char* lds, float* __restrict__ slab) {
+    using namespace w3;
+    constexpr int MT = (WA / WM + 31) / 32, NT = (WB / WN + 31) / 32;
+    constexpr int M = WA, N = WB;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool active = wave < WM * WN;
+    const int mi = wave / WN, ni = wave % WN;
+    const int m0 = 32 * MT * mi, n0 = 32 * NT * ni;
+    const int h = lane >> 5, col = lane & 31;
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x16{};
+    float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+
+    // two register sets per operand: the loads run two stages ahead
+    Stager<KA, WA> sa[2];
+    Stager<KB, WB> sb[2];
+    sa[0].init(tid); sa[1].init(tid);
+    sb[0].init(tid); sb[1].init(tid);
+    if constexpr (KA == SEG_HEAD) {     // rows 4..31 of the 4-row gradient image stay 0
+        for (int i = tid; i < 2 * 3 * 32 * kColB / 4; i += kThreads) {
+            const int b = i / (3 * 32 * kColB / 4), r = i % (3 * 32 * kColB / 4);
+            const int p = r / (32 * kColB / 4), o = r % (32 * kColB / 4);
+            reinterpret_cast<uint32_t*>(lds + b * kBufB + p * kPlane)[o] = 0u;
+        }
+        __syncthreads();
+    }
+    const int nst = 2 * (b1 - b0);      // half-block stages
+    // stages past the end load a valid block and store zeros into a buffer
+    // nobody reads again
+    const int blast = b1 > b0 ? b1 - 1 : b0;
+    auto load = [&](int set, int st) {
+        const int blk = min(b0 + (st >> 1), blast), hb = st & 1;
+        sa[set].load(T.a.base, blk, hb);
+        sb[set].load(T.b.base, blk, hb);
+    };
+    auto store = [&](int set, int buf, int st) {
+        const int nval = st < nst ? a.n - (b0 + (st >> 1)) * 32 - 16 * (st & 1) : 0;
+        float sdummy[4] = {0.f, 0.f, 0.f, 0.f};
+        sa[set].store(lds + buf * kBufB, nval, bacc);
+        sb[set].store(lds + buf * kBufB + kOpnd, nval, sdummy);
+    };
+    // LDS-only barrier: keeps the prefetched global loads in flight
+    auto barrier = [] {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    auto compute = [&](int buf) {
+        if constexpr (WM * WN < 8) {
+            if (!active) return;
+        }
+        const char* la = lds + buf * kBufB + (m0 + col) * kColB + 16 * h;
+        const char* lb = lds + buf * kBufB + kOpnd + (n0 + col) * kColB + 16 * h;
+        x3::Pieces bp[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            bp[j].hi = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB);
+            bp[j].mid = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB + kPlane);
+            bp[j].lo = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB + 2 * kPlane);
+        }
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const x3::bf16x8 ah = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB);
+            const x3::bf16x8 am = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB + kPlane);
+            const x3::bf16x8 al = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB + 2 * kPlane);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = x3::mfma_x6(ah, am, al, bp[j], acc[i][j]);
+        }
+    };
+    // stage st lives in LDS buffer st & 1 and register set st & 1
+    load(0, 0);
+    load(1, 1);
+    store(0, 0, 0);
+    barrier();
+#pragma unroll 1
+    for (int st = 0; st < nst; st += 2) {
+        load(0, st + 2);              // set 0 is free again (stage st is in LDS)
+        compute(0);
+        store(1, 1, st + 1);
+        barrier();
+        load(1, st + 3);
+        compute(1);
+        store(0, 0, st + 2);
+        barrier();
+    }
+    // bias sums: reduce the 8 sample pairs of each (chunk, half) group of the
+    // gradient operand; lane jp == 0 writes
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        bacc[e] += __shfl_xor(bacc[e], 1);
+        bacc[e] += __shfl_xor(bacc[e], 2);
+        bacc[e] += __shfl_xor(bacc[e], 4);
+    }
+    if (sa[0].act && sa[0].jp == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int o = KA == SEG_HEAD ? e : Geo3<KA, WA>::col(sa[0].k, sa[0].h) + e;
+            if (o < M) slab[M * N + o] = bacc[e];
+        }
+    }
+    if (!active) return;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = m0 + 32 * i + nr_acc_row(r, h);
+                const int c = n0 + 32 * j + col;
+                if (o < M && c < N) slab[o * N + c] = acc[i][j][r];
+            }
+}
+
+__global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[w3::kLds];
+    int t = 0;
+#pragma unroll 1
+    while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
+    const WgTask& T = a.task[t];
+    const int c = blockIdx.x - a.wg_start[t];
+    const int b0 = (int)((int64_t)c * a.nb / T.G);
+    const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
+    float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
+    switch (__builtin_amdgcn_readfirstlane(T.id)) {
+        case 0: case 4:
+            wgrad3_body<SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
+        case 10:
+            wgrad3_body<SEG_ACC, 128, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
+        case 11:
+            wgrad3_body<SEG_ACC, 128, SEG_DPE, 32, 4, 1>(a, T, b0, b1, lds, slab); break;
+        case 12:
+            wgrad3_body<SEG_HEAD, 4, SEG_ACC, 256, 1, 8>(a, T, b0, b1, lds, slab); break;
+        case 13:
+            wgrad3_body<SEG_HEAD, 4, SEG_ACC, 128, 1, 4>(a, T, b0, b1, lds, slab); break;
+        default:
+            wgrad3_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
+    }
+}
+
 // destination of output element (o, c) of task t in the flat gradient (-1 = none)
 __device__ int wgrad_dest(int t, int o, int c) {
     switch (t) {
@@ -309,8 +534,9 @@ NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
     return (int64_t)(3 * kTargetWG + kTasks) * (256 * 256 + 256) * sizeof(float);
 }
 
-NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
-                    float* grad_flat, void* stream) {
+namespace {
+int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, float* workspace,
+                 float* grad_flat, void* stream) {
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_wgrad: n out of range");
     NR_REQUIRE(save && grad_ws && workspace && grad_flat, "nr_wgrad: null pointer");
     NR_REQUIRE((((uintptr_t)save | (uintptr_t)grad_ws) & 15) == 0,
@@ -340,24 +566,26 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
     };
     WgArgs a{};
     // per-block cost of a task's workgroup, in cycles: the MFMA time of its
-    // busiest SIMD, or the staging of (M + N) x 32 floats at ~8 B/cycle per CU,
-    // plus a fixed barrier/LDS-store overhead
+    // busiest SIMD (fp32: 16 k-steps x 64 cycles per tile; bf16x6: 2 x 6 x 32),
+    // or the staging of (M + N) x 32 floats at ~8 B/cycle per CU, plus a fixed
+    // barrier/LDS-store overhead
     int64_t cost[kTasks], tot = 0;
     for (int t = 0; t < kTasks; ++t) {
         const int mt = (tasks[t].a.width / tasks[t].wm + 31) / 32;
         const int nt = (tasks[t].b.width / tasks[t].wn + 31) / 32;
-        const int64_t mfma = 16 * mt * nt * 64 * (tasks[t].wm * tasks[t].wn > 4 ? 2 : 1);
+        const int64_t per_tile = x3 ? 384 : 1024;
+        const int64_t mfma = per_tile * mt * nt * (tasks[t].wm * tasks[t].wn > 4 ? 2 : 1);
         const int64_t bytes = (int64_t)(tasks[t].a.width + tasks[t].b.width) * 32 * 4;
         cost[t] = std::max<int64_t>(mfma, bytes / 8) + 512;
         tot += cost[t];
     }
-    // dispatch order: the heavy 256x256 tasks first; the small, memory-bound
-    // tasks last and split ~3x finer, so their short workgroups fill the tail
-    // of the final round
+    // dispatch order: the heavy tasks first; the small ones last and split ~3x
+    // finer, so their short workgroups fill the tail of the final round
+    const int64_t heavy = x3 ? 6144 : 16384;
     int order[kTasks], no = 0;
     for (int pass = 0; pass < 2; ++pass)
         for (int t = 0; t < kTasks; ++t)
-            if ((cost[t] >= 16384) == (pass == 0)) order[no++] = t;
+            if ((cost[t] >= heavy) == (pass == 0)) order[no++] = t;
     a.wg_start[0] = 0;
     int64_t slab = 0;
     // diagnostic: NR_WGRAD_TASKMASK limits the launch to a subset of task ids
@@ -366,7 +594,7 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
         getenv("NR_WGRAD_TASKMASK") ? strtoll(getenv("NR_WGRAD_TASKMASK"), nullptr, 0) : -1;
     for (int k = 0; k < kTasks; ++k) {
         const int t = order[k];
-        const int split = cost[t] >= 16384 ? 1 : 3;
+        const int split = cost[t] >= heavy ? 1 : 3;
         int64_t g = split * ((kTargetWG * cost[t] + tot - 1) / tot);
         g = std::max<int64_t>(1, std::min<int64_t>(g, nb));
         if (!((tmask >> t) & 1)) g = 0;
@@ -380,10 +608,22 @@ NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* w
     a.nb = (int)nb;
     a.n = (int)n;
     a.slab = workspace;
-    wgrad_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    if (x3) wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else wgrad_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     NR_LAUNCH_CHECK("nr_wgrad");
     dim3 rg((256 * 256 + 256 + 255) / 256, kTasks);
     wgrad_reduce_kernel<<<rg, 256, 0, st>>>(a, grad_flat);
     NR_LAUNCH_CHECK("nr_wgrad_reduce");
     return 0;
+}
+}  // namespace
+
+NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                    float* grad_flat, void* stream) {
+    return wgrad_launch(false, save, grad_ws, n, workspace, grad_flat, stream);
+}
+
+NR_API int nr_wgrad_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                       float* grad_flat, void* stream) {
+    return wgrad_launch(true, save, grad_ws, n, workspace, grad_flat, stream);
 }

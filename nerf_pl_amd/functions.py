@@ -66,7 +66,8 @@ class _FusedMLP(torch.autograd.Function):
              g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), stream_of(dev))
         gflat = torch.empty(packing.N_PARAMS, device=dev)
         ws = _wgrad_workspace(dev.index)
-        call("nr_wgrad", save.data_ptr(), grad_ws.data_ptr(), n, ws.data_ptr(),
+        call("nr_wgrad_x3" if ops.MATH == "bf16x6" else "nr_wgrad", save.data_ptr(),
+             grad_ws.data_ptr(), n, ws.data_ptr(),
              gflat.data_ptr(), stream_of(dev))
         grads, off = [], 0
         for name, shp in _SHAPES:

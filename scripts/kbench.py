@@ -13,7 +13,7 @@ from nerf_pl_amd._lib import call, stream_of
 from nerf_pl_amd.functions import _wgrad_workspace
 
 FLOP = {"fwd": 1186816, "fwdsave": 1186816, "fwd3": 1186816, "fwd3save": 1186816,
-        "bwd": 1115392, "bwd3": 1115392, "wgrad": 1186816}
+        "bwd": 1115392, "bwd3": 1115392, "wgrad": 1186816, "wgrad3": 1186816}
 PEAK3 = 2516.6 / 6     # bf16 dense MFMA peak / 6 products: fp32-equivalent ceiling of bf16x6
 
 
@@ -57,10 +57,12 @@ def main():
         elif k == "bwd3":
             call("nr_mlp_bwd_x3", pb3.data_ptr(), ops.head_ptr(p3), out.data_ptr(), gout.data_ptr(),
                  sv.data_ptr(), n, gw.data_ptr(), st)
+        elif k == "wgrad3":
+            call("nr_wgrad_x3", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
         elif k == "wgrad":
             call("nr_wgrad", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
 
-    ks = ["fwd", "fwdsave", "fwd3", "fwd3save", "bwd", "bwd3", "wgrad"] if which == "all" \
+    ks = ["fwd", "fwdsave", "fwd3", "fwd3save", "bwd", "bwd3", "wgrad", "wgrad3"] if which == "all" \
         else which.split(",")
     run("bwd")
     for k in ks:

@@ -5,7 +5,9 @@ import glob
 import sys
 
 d = sys.argv[1]
-TAGS = [("mlp_fwd_kernel", "mlp_fwd"), ("mlp_bwd_kernel", "mlp_bwd"),
+FWD_SPLIT = len(sys.argv) > 2 and sys.argv[2] == "split"
+TAGS = [("mlp_fwd3_kernel", "mlp_fwd3"), ("mlp_bwd3_kernel", "mlp_bwd3"),
+        ("wgrad3_kernel", "wgrad3"), ("mlp_fwd_kernel", "mlp_fwd"), ("mlp_bwd_kernel", "mlp_bwd"),
         ("wgrad_kernel", "wgrad"), ("wgrad_reduce", "wgrad_reduce")]
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 dur = collections.defaultdict(list)
@@ -23,8 +25,8 @@ for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
             seen[tag] += 1
             order[did] = seen[tag]
         k = tag
-        if tag == "mlp_fwd":   # kbench order: 5 fwd (no save) then 5 fwd+save
-            k = "mlp_fwd" if order[did] <= 5 else "mlp_fwd+save"
+        if tag in ("mlp_fwd", "mlp_fwd3") and FWD_SPLIT:   # kbench: 5 fwd then 5 fwd+save
+            k = tag if order[did] <= 5 else tag + "+save"
         vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
 for k, cs in vals.items():
