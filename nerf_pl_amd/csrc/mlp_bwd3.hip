@@ -80,6 +80,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     const f32x4 yo = *reinterpret_cast<const f32x4*>(a.out + (size_t)s * 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // masks (and the prologue) landed
     const uint4* mask = smask + lane;                   // [layer * 64]
+    Frag f0;                                            // tile-0 fragments of the next k-group
+    enter<BwdTab, 0, kQ>(smem, lane, f0);
 
     float dzr[3];
 #pragma unroll
@@ -136,7 +138,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
             store_native_piece<4>(reinterpret_cast<const f32x16(&)[4]>(C), 2 * g, cdst, lane);
             store_native_piece<4>(reinterpret_cast<const f32x16(&)[4]>(C), 2 * g + 1, cdst, lane);
         };
-        segment<BwdTab, kDirT, 0, 8, 8, kQ>(PB, smem, wave, lane, A, gb, sd);
+        segment<BwdTab, kDirT, 0, 8, 8, kQ>(PB, smem, wave, lane, A, gb, sd, f0);
     }
     // d h8 = W_final^T dfeat + W_sigma^T dsigma, masked by h8; stores dfeat
 #pragma unroll
@@ -151,7 +153,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         const uint4 mk = mask[7 * 64];
         auto gb = from_acc(A);
         auto sd = side8(A, dzseg(8));
-        segment<BwdTab, kFinalT, 0, 16, 8, kQ>(PB, smem, wave, lane, B, gb, sd);
+        segment<BwdTab, kFinalT, 0, 16, 8, kQ>(PB, smem, wave, lane, B, gb, sd, f0);
         relu_mask<8>(B, mk);
     }
 #define NR_BACK3(DST, SRC, Q0, L)                                              \
@@ -160,7 +162,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         zero<8>(DST);                                                          \
         auto gb = from_acc(SRC);                                               \
         auto sd = side8(SRC, dzseg(L));                                        \
-        segment<BwdTab, Q0, 0, 16, 8, kQ>(PB, smem, wave, lane, DST, gb, sd);  \
+        segment<BwdTab, Q0, 0, 16, 8, kQ>(PB, smem, wave, lane, DST, gb, sd, f0); \
         relu_mask<8>(DST, mk);                                                 \
     }
     NR_BACK3(A, B, kL8T, 7)   // dz7 = (W8^T dz8) * [h7 > 0], stores dz8

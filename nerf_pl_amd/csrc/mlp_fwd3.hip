@@ -143,6 +143,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     }
     prologue<FwdTab, QEND>(P, smem, wave, lane);
     __syncthreads();   // head visible (the DMA stays in flight: waited per group)
+    Frag f0;           // tile-0 fragments of the next k-group
+    enter<FwdTab, 0, QEND>(smem, lane, f0);
     const float* H = Hs;
     const int nb = (a.n + 31) / 32;
     const bool save = a.save != nullptr && blk < nb;
@@ -208,7 +210,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
                 *reinterpret_cast<f32x4*>(pdst + (grp * 64 + lane) * 4) = v;
             }
         };
-        segment<FwdTab, kL1, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, side);
+        segment<FwdTab, kL1, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, side, f0);
         relu<8>(A);
     }
 #define NR_DENSE3(DST, SRC, Q0, L)                                              \
@@ -216,7 +218,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         init_bias<8>(DST, H + NR_H_BIAS(L), h);                                 \
         auto gb = from_acc(SRC);                                                \
         auto sd = side_acc(SRC, hseg(L - 2), mseg(L - 2));                      \
-        segment<FwdTab, Q0, 0, 16, 8, QEND>(P, smem, wave, lane, DST, gb, sd);          \
+        segment<FwdTab, Q0, 0, 16, 8, QEND>(P, smem, wave, lane, DST, gb, sd, f0);      \
         relu<8>(DST);                                                           \
     }
     NR_DENSE3(B, A, kL2, 2)
@@ -232,10 +234,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = pe[8 * g + j];
         };
-        segment<FwdTab, kL5, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, none);
+        segment<FwdTab, kL5, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, none, f0);
         auto gb = from_acc(B);
         auto sd = side_acc(B, hseg(3), mseg(3));
-        segment<FwdTab, kL5 + 4, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd);
+        segment<FwdTab, kL5 + 4, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd, f0);
         relu<8>(A);
     }
     NR_DENSE3(B, A, kL6, 6)
@@ -252,7 +254,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             init_bias<8>(A, H + NR_H_BFINAL, h);
             auto gb = from_acc(B);
             auto sd = side_acc(B, hseg(7), mseg(7));
-            segment<FwdTab, kFinal, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd);
+            segment<FwdTab, kFinal, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd, f0);
         }
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
         float dpe[NR_DIR_KSTEPS];
@@ -264,7 +266,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             float* fdst = SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256);
             auto gb = from_acc(A);
             auto sd = side_acc(A, fdst, nullptr);
-            segment<FwdTab, kDir, 0, 16, 4, QEND>(P, smem, wave, lane, C, gb, sd);
+            segment<FwdTab, kDir, 0, 16, 4, QEND>(P, smem, wave, lane, C, gb, sd, f0);
         }
         {
             float* ddst = SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32);
@@ -283,7 +285,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
                     *reinterpret_cast<f32x4*>(ddst + (grp * 64 + lane) * 4) = v;
                 }
             };
-            segment<FwdTab, kDir + 16, 0, 2, 4, QEND>(P, smem, wave, lane, C, getb, side);
+            segment<FwdTab, kDir + 16, 0, 2, 4, QEND>(P, smem, wave, lane, C, getb, side, f0);
         }
         relu<4>(C);
         float rgb[3];

@@ -10,6 +10,12 @@
 #include <utility>
 #include "layout.h"
 
+// NR_X3_DBG (timing experiments only, never in the shipped build):
+// 1 = no barrier, 2 = no DMA wait and no barrier, 3 = no DMA at all
+#ifndef NR_X3_DBG
+#define NR_X3_DBG 0
+#endif
+
 namespace x3 {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -43,7 +49,7 @@ __device__ __forceinline__ char* slot_ptr(char* ring, int q) { return ring + (q 
 template <class TAB, int Q, int QEND>
 __device__ __forceinline__ void stage(const char* __restrict__ packed, char* ring, int wave,
                                       int lane) {
-    if constexpr (Q < QEND) {
+    if constexpr (Q < QEND && NR_X3_DBG != 3) {
         constexpr int NT = TAB::tiles(Q);
         const char* src = packed + TAB::off(Q);
         char* dst = slot_ptr(ring, Q);
@@ -65,12 +71,15 @@ __device__ __forceinline__ void prologue(const char* __restrict__ packed, char* 
     stage<TAB, 1, QEND>(packed, ring, wave, lane);
     stage<TAB, 2, QEND>(packed, ring, wave, lane);
 }
+// forward declaration order: enter<> is defined below; kernels call
+// enter<TAB, 0, QEND>(ring, lane, f0) once after the prologue.
 
 // group Q may be read once this wave's DMA landed and every wave passed here
 template <class TAB, int Q, int QEND>
 __device__ __forceinline__ void ring_enter() {
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(wait_count<TAB, Q, QEND>()) : "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr (NR_X3_DBG < 2)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(wait_count<TAB, Q, QEND>()) : "memory");
+    if constexpr (NR_X3_DBG == 0) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
 
@@ -106,16 +115,52 @@ __device__ __forceinline__ f32x16 mfma_x6(const bf16x8& ah, const bf16x8& am, co
     return acc;
 }
 
-// one k-group: acc[t] += W_q[t] * B for the NT output tiles
+// pin a value to this point of the instruction stream (the compiler would
+// otherwise sink the next group's split down to its first use, after the
+// barrier, where nothing hides it)
+__device__ __forceinline__ void pin(Pieces& p) {
+    asm volatile("" : "+v"(p.hi), "+v"(p.mid), "+v"(p.lo));
+}
+
+// the three weight pieces of one output tile of a k-group
+struct Frag { bf16x8 p[3]; };
+
 template <int Q, int NT>
-__device__ __forceinline__ void group_mm(char* ring, int lane, f32x16 (&acc)[8], const Pieces& b) {
-    const char* s = slot_ptr(ring, Q) + lane * 16;
+__device__ __forceinline__ void rd_frag(char* ring, int lane, int t, Frag& f) {
+    const char* s = slot_ptr(ring, Q) + lane * 16 + t * 1024;
+    f.p[0] = *reinterpret_cast<const bf16x8*>(s);
+    f.p[1] = *reinterpret_cast<const bf16x8*>(s + NT * 1024);
+    f.p[2] = *reinterpret_cast<const bf16x8*>(s + 2 * NT * 1024);
+}
+
+// hand group Q over (wait + barrier) and read its tile-0 fragments
+template <class TAB, int Q, int QEND>
+__device__ __forceinline__ void enter(char* ring, int lane, Frag& f0) {
+    if constexpr (Q < QEND) {
+        ring_enter<TAB, Q, QEND>();
+        rd_frag<Q, TAB::tiles(Q)>(ring, lane, 0, f0);
+    }
+}
+
+// one k-group: acc[t] += W_q[t] * B for the NT output tiles.  On entry f0
+// holds tile 0 of group Q; the fragments of tile t+1 are read while tile t
+// multiplies, and the hand-over of group Q+1 (wait, barrier, its tile-0 read)
+// is done before the last tile's MFMAs, so both the barrier and the first LDS
+// latency of the next group hide under MFMAs in flight.  On exit f0 holds
+// tile 0 of group Q+1.  hook(t) runs after tile t's MFMAs are issued.
+template <class TAB, int Q, int NT, int QEND, typename Hook>
+__device__ __forceinline__ void group_mm(char* ring, int lane, f32x16 (&acc)[8], const Pieces& b,
+                                         Hook& hook, Frag& f0) {
+    Frag f[2];
+    f[0] = f0;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(s + (0 * NT + t) * 1024);
-        const bf16x8 am = *reinterpret_cast<const bf16x8*>(s + (1 * NT + t) * 1024);
-        const bf16x8 al = *reinterpret_cast<const bf16x8*>(s + (2 * NT + t) * 1024);
-        acc[t] = mfma_x6(ah, am, al, b, acc[t]);
+        if (t + 1 < NT) rd_frag<Q, NT>(ring, lane, t + 1, f[(t + 1) & 1]);
+        if (t == NT - 1) enter<TAB, Q + 1, QEND>(ring, lane, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        acc[t] = mfma_x6(f[t & 1].p[0], f[t & 1].p[1], f[t & 1].p[2], b, acc[t]);
+        hook(t);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -123,20 +168,41 @@ __device__ __forceinline__ void group_mm(char* ring, int lane, f32x16 (&acc)[8],
 // recursion: ring slots, DMA sources and wait counts are constants).
 //   getb(IC<g>, float (&x)[8]): the 8 fp32 B values of local group g
 //   side(IC<g>): output stores of the previous layer, spread over the groups
+// b holds the pieces of group G (split one group ahead, inside group G-1);
+// f0 carries the next group's tile-0 fragments across groups and segments.
 template <class TAB, int Q0, int G, int NG, int NT, int QEND, typename GetB, typename Side>
-__device__ __forceinline__ void segment(const char* __restrict__ packed, char* ring, int wave,
-                                        int lane, f32x16 (&acc)[8], GetB& getb, Side& side) {
+__device__ __forceinline__ void segment_from(const char* __restrict__ packed, char* ring, int wave,
+                                             int lane, f32x16 (&acc)[8], GetB& getb, Side& side,
+                                             const Pieces& b, Frag& f0) {
     if constexpr (G < NG) {
         constexpr int Q = Q0 + G;
-        ring_enter<TAB, Q, QEND>();
-        stage<TAB, Q + kSlots - 1, QEND>(packed, ring, wave, lane);
-        side(IC<G>());
-        float x[8];
-        getb(IC<G>(), x);
-        const Pieces b = split8(x);
-        group_mm<Q, NT>(ring, lane, acc, b);
-        segment<TAB, Q0, G + 1, NG, NT, QEND>(packed, ring, wave, lane, acc, getb, side);
+        Pieces bn = b;
+        auto hook = [&](int t) {
+            if (t == 0) stage<TAB, Q + kSlots - 1, QEND>(packed, ring, wave, lane);
+            if (t == 1) {
+                if constexpr (G + 1 < NG) {
+                    float x[8];
+                    getb(IC<G + 1>(), x);
+                    bn = split8(x);
+                    pin(bn);
+                }
+            }
+            if (t == 2) side(IC<G>());
+        };
+        group_mm<TAB, Q, NT, QEND>(ring, lane, acc, b, hook, f0);
+        segment_from<TAB, Q0, G + 1, NG, NT, QEND>(packed, ring, wave, lane, acc, getb, side, bn,
+                                                   f0);
     }
+}
+
+template <class TAB, int Q0, int G, int NG, int NT, int QEND, typename GetB, typename Side>
+__device__ __forceinline__ void segment(const char* __restrict__ packed, char* ring, int wave,
+                                        int lane, f32x16 (&acc)[8], GetB& getb, Side& side,
+                                        Frag& f0) {
+    float x[8];
+    getb(IC<0>(), x);
+    const Pieces b = split8(x);
+    segment_from<TAB, Q0, 0, NG, NT, QEND>(packed, ring, wave, lane, acc, getb, side, b, f0);
 }
 
 // B values of k-group g of a 256-wide accumulator input (packing.kmap3)
