@@ -12,15 +12,21 @@ import json
 import sys
 
 d, out = sys.argv[1], sys.argv[2]
-TAGS = [("mlp_fwd_kernel", "mlp_fwd"), ("mlp_bwd_kernel", "mlp_bwd_dgrad"),
+X3_ONLY = "--x3" in sys.argv[3:]
+# the bf16x6 kernels (the default arithmetic) and the fp32 ones map to the
+# same bench tags; profile one arithmetic per run
+TAGS = [("mlp_fwd3_kernel", "mlp_fwd"), ("mlp_bwd3_kernel", "mlp_bwd_dgrad"),
+        ("wgrad3_kernel", "mlp_wgrad"),
+        ("mlp_fwd_kernel", "mlp_fwd"), ("mlp_bwd_kernel", "mlp_bwd_dgrad"),
         ("wgrad_reduce", "wgrad_reduce"), ("wgrad_kernel", "mlp_wgrad")]
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
     order, seen = {}, collections.Counter()
     for r in csv.DictReader(open(f)):
-        tag = next((t for s, t in TAGS if s in r["Kernel_Name"]), None)
-        if tag is None:
+        hit = next(((s_, t) for s_, t in TAGS if s_ in r["Kernel_Name"]), None)
+        if hit is None or (X3_ONLY and "3_kernel" not in hit[0] and "reduce" not in hit[0]):
             continue
+        tag = hit[1]
         did = int(r["Dispatch_Id"])
         if did not in order:
             seen[tag] += 1
@@ -36,6 +42,7 @@ for k, cs in vals.items():
         write = med["WRITE_SIZE"] * 1024
         res[k] = {"samples": 786432, "fetch_bytes": fetch, "write_bytes": write,
                   "hbm_bytes": fetch + write,
+                  "arithmetic": "bf16x6" if X3_ONLY else "fp32",
                   "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes; "
                             "FETCH_SIZE x2 (gfx950 wide-stream correction)"}
 json.dump(res, open(out, "w"), indent=1)
