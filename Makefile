@@ -2,7 +2,7 @@
 # and the C pieces of the oracle.  `make -j8`
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-HIPFLAGS ?= -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -Wall -Wno-unused-function
+HIPFLAGS ?= -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize --offload-arch=$(ARCH) -Wall -Wno-unused-function
 SRC := $(wildcard nerf_pl_amd/csrc/*.hip)
 HDR := $(wildcard nerf_pl_amd/csrc/*.h)
 OBJ := $(patsubst nerf_pl_amd/csrc/%.hip,build/%.o,$(SRC))

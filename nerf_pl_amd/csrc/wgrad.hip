@@ -263,6 +263,17 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
 // (column stride 48 B: conflict-free ds_read_b128 fragments), double
 // buffered; the bias sums come from the fp32 values during staging.
 // ---------------------------------------------------------------------------
+// NR_W3_DBG (timing experiments only): 1 = no MFMAs, 2 = no global loads after
+// the first stage, 3 = no LDS staging stores
+#ifndef NR_W3_DBG
+#define NR_W3_DBG 0
+#endif
+#ifndef NR_W3_SGB
+#define NR_W3_SGB 1
+#endif
+#ifndef NR_W3_MULTI
+#define NR_W3_MULTI 1
+#endif
 namespace w3 {
 constexpr int kColB = 48;                        // bytes per column (16 bf16 + pad)
 constexpr int kPlane = 256 * kColB;              // one piece of one operand
@@ -287,12 +298,13 @@ struct Stager {
     bool act;      // this thread owns a pair (loads run for every thread, clamped)
     int k, h, jp;  // chunk, lane half, sample pair
     f32x4 v0, v1;
+    static constexpr bool ALL = KIND != SEG_HEAD && Geo3<KIND, W>::CHUNKS * 16 >= kThreads;
     __device__ __forceinline__ void init(int tid) {
         if constexpr (KIND == SEG_HEAD) {
             act = tid < 8; k = 0; h = 0; jp = tid & 7;
         } else {
             k = tid >> 4; h = (tid >> 3) & 1; jp = tid & 7;
-            act = k < Geo3<KIND, W>::CHUNKS;
+            act = ALL || k < Geo3<KIND, W>::CHUNKS;
             k = act ? k : 0;
         }
     }
@@ -309,28 +321,20 @@ struct Stager {
             v0 = p[0]; v1 = p[1];
         }
     }
-    // split + store into an operand image; samples >= nval become 0; adds the
-    // per-column sums of the two samples (bias) to s[e]
-    __device__ __forceinline__ void store(char* img, int nval, float (&s)[4]) {
-        if (!act) return;
+    // split + store column e of this thread's chunk into an operand image;
+    // samples >= nval become 0; adds the two samples' sum (bias) to s
+    __device__ __forceinline__ void store_e(char* img, int nval, int e, float& s) {
+        if (!ALL && !act) return;
         const int j = 2 * jp;
-        const f32x4 a = j < nval ? v0 : f32x4{};
-        const f32x4 b = j + 1 < nval ? v1 : f32x4{};
+        const float x0 = j < nval ? v0[e] : 0.f, x1 = j + 1 < nval ? v1[e] : 0.f;
         const int c0 = KIND == SEG_HEAD ? 0 : Geo3<KIND, W>::col(k, h);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const x3::f32x2 x = {a[e], b[e]};
-            s[e] += x[0] + x[1];
-            const x3::bf16x2 hi = __builtin_convertvector(x, x3::bf16x2);
-            const x3::f32x2 r1 = x - __builtin_convertvector(hi, x3::f32x2);
-            const x3::bf16x2 mid = __builtin_convertvector(r1, x3::bf16x2);
-            const x3::bf16x2 lo = __builtin_convertvector(r1 - __builtin_convertvector(mid, x3::f32x2),
-                                                          x3::bf16x2);
-            char* q = img + (c0 + e) * kColB + 4 * jp;
-            *reinterpret_cast<x3::bf16x2*>(q) = hi;
-            *reinterpret_cast<x3::bf16x2*>(q + kPlane) = mid;
-            *reinterpret_cast<x3::bf16x2*>(q + 2 * kPlane) = lo;
-        }
+        s += x0 + x1;
+        x3::bf16x2 hi, mid, lo;
+        x3::split2(x0, x1, hi, mid, lo);
+        char* q = img + (c0 + e) * kColB + 4 * jp;
+        *reinterpret_cast<x3::bf16x2*>(q) = hi;
+        *reinterpret_cast<x3::bf16x2*>(q + kPlane) = mid;
+        *reinterpret_cast<x3::bf16x2*>(q + 2 * kPlane) = lo;
     }
 };
 }  // namespace w3
@@ -372,15 +376,19 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
     // nobody reads again
     const int blast = b1 > b0 ? b1 - 1 : b0;
     auto load = [&](int set, int st) {
+        if (NR_W3_DBG == 2 && st > 1) return;
         const int blk = min(b0 + (st >> 1), blast), hb = st & 1;
         sa[set].load(T.a.base, blk, hb);
         sb[set].load(T.b.base, blk, hb);
     };
     auto store = [&](int set, int buf, int st) {
         const int nval = st < nst ? a.n - (b0 + (st >> 1)) * 32 - 16 * (st & 1) : 0;
-        float sdummy[4] = {0.f, 0.f, 0.f, 0.f};
-        sa[set].store(lds + buf * kBufB, nval, bacc);
-        sb[set].store(lds + buf * kBufB + kOpnd, nval, sdummy);
+        float sdummy = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            sa[set].store_e(lds + buf * kBufB, nval, e, bacc[e]);
+            sb[set].store_e(lds + buf * kBufB + kOpnd, nval, e, sdummy);
+        }
     };
     // LDS-only barrier: keeps the prefetched global loads in flight
     auto barrier = [] {
@@ -388,42 +396,83 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-    auto compute = [&](int buf) {
-        if constexpr (WM * WN < 8) {
-            if (!active) return;
-        }
+    // compute stage (buffer buf) from LDS while staging the next stage from
+    // register set `set` into buffer buf ^ 1: the 8 store units (2 operands x
+    // 4 columns) are spread between the row tiles' MFMAs so their VALU and
+    // LDS-store work overlaps the MFMAs in flight instead of idling both waves
+    // of a SIMD at the same time
+    auto compute_store = [&](int buf, int set, int st_next) {
+        const int nval = st_next < nst ? a.n - (b0 + (st_next >> 1)) * 32 - 16 * (st_next & 1) : 0;
+        char* ia = lds + (buf ^ 1) * kBufB;
+        char* ib = ia + kOpnd;
+        float sdummy = 0.f;
+        auto unit = [&](int u) {
+            if (NR_W3_DBG == 3) return;
+            if (u < 4) sa[set].store_e(ia, nval, u, bacc[u]);
+            else sb[set].store_e(ib, nval, u - 4, sdummy);
+        };
         const char* la = lds + buf * kBufB + (m0 + col) * kColB + 16 * h;
         const char* lb = lds + buf * kBufB + kOpnd + (n0 + col) * kColB + 16 * h;
+        const bool go = (WM * WN == 8 || active) && NR_W3_DBG != 1;
         x3::Pieces bp[NT];
+        if (go) {
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            bp[j].hi = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB);
-            bp[j].mid = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB + kPlane);
-            bp[j].lo = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB + 2 * kPlane);
+            for (int j = 0; j < NT; ++j) {
+                bp[j].hi = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB);
+                bp[j].mid = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB + kPlane);
+                bp[j].lo = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB + 2 * kPlane);
+            }
         }
+        constexpr int UPT = (8 + MT - 1) / MT;   // store units per row tile
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
-            const x3::bf16x8 ah = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB);
-            const x3::bf16x8 am = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB + kPlane);
-            const x3::bf16x8 al = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB + 2 * kPlane);
+            if (go) {
+                const x3::bf16x8 ah = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB);
+                const x3::bf16x8 am = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB + kPlane);
+                const x3::bf16x8 al = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB + 2 * kPlane);
+#if NR_W3_MULTI
+                x3::mfma_x6_multi<NT>(ah, am, al, bp, acc[i]);
+#else
 #pragma unroll
-            for (int j = 0; j < NT; ++j) acc[i][j] = x3::mfma_x6(ah, am, al, bp[j], acc[i][j]);
+                for (int j = 0; j < NT; ++j) acc[i][j] = x3::mfma_x6(ah, am, al, bp[j], acc[i][j]);
+#endif
+            }
+#pragma unroll
+            for (int v = 0; v < UPT; ++v)
+                if (i * UPT + v < 8) unit(i * UPT + v);
         }
+#if NR_W3_SGB
+        // interleave: per row tile, its fragment reads, then each MFMA followed
+        // by two VALU ops of the store units, then the units' LDS stores
+        if constexpr (WM * WN == 8) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 3 * NT, 0);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+                for (int r = 0; r < 6 * NT; ++r) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, NR_W3_SGB, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x200, 3 * UPT, 0);
+            }
+        }
+#endif
     };
-    // stage st lives in LDS buffer st & 1 and register set st & 1
+    // stage st lives in LDS buffer st & 1 and register set st & 1; a set is
+    // reloaded (two stages ahead) as soon as its stage has been stored
     load(0, 0);
     load(1, 1);
     store(0, 0, 0);
+    load(0, 2);
     barrier();
 #pragma unroll 1
     for (int st = 0; st < nst; st += 2) {
-        load(0, st + 2);              // set 0 is free again (stage st is in LDS)
-        compute(0);
-        store(1, 1, st + 1);
-        barrier();
+        compute_store(0, 1, st + 1);  // stage st from buffer 0; set 1 (stage st+1) -> buffer 1
         load(1, st + 3);
-        compute(1);
-        store(0, 0, st + 2);
+        barrier();
+        compute_store(1, 0, st + 2);  // stage st+1 from buffer 1; set 0 (stage st+2) -> buffer 0
+        load(0, st + 4);
         barrier();
     }
     // bias sums: reduce the 8 sample pairs of each (chunk, half) group of the
