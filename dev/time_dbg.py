@@ -18,7 +18,8 @@ out, sv = ops.mlp_forward(p3, rays=rays, z=z, samples_per_ray=spr, save=True)
 gout = torch.randn(n, 4, device=dev)
 gw = torch.empty(ops.n_blocks(n) * ops.GRAD_PER_BLOCK, device=dev)
 st = stream_of(dev)
-for v in range(4):
+VARIANTS = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1", "2", "3", "4", "5", "s0", "s2", "8"]
+for v in VARIANTS:
     L = ctypes.CDLL(os.path.abspath(f"dev/libx3dbg{v}.so"))
     f = L.nr_mlp_fwd_x3
     f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
@@ -30,6 +31,22 @@ for v in range(4):
         "fwd3save": lambda: f(p3.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0, out.data_ptr(), sv.data_ptr(), st),
         "bwd3": lambda: b(pb3.data_ptr(), ops.head_ptr(p3), out.data_ptr(), gout.data_ptr(), sv.data_ptr(), n, gw.data_ptr(), st),
     }
+    if v == "8":   # clock stamps: full forward, no save; stamps written through the save pointer
+        nb = (n + 31) // 32
+        stp = torch.zeros(nb * 4, dtype=torch.int64, device=dev)
+        for _ in range(20):
+            f(p3.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0, out.data_ptr(), stp.data_ptr(), st)
+        torch.cuda.synchronize()
+        w = stp.view(nb, 4).cpu().double()
+        dt_real = w[:, 1] - w[:, 0]
+        clock = w[:, 2] / dt_real.clamp(min=1) * 100
+        span = (w[:, 1].max() - w[:, 0].min()).item() / 100
+        busy = dt_real.sum().item() / 100 / 1024
+        print(f"dbg8 clock median {clock.median().item():.0f} MHz (p10 {clock.quantile(0.1).item():.0f}); "
+              f"wave median {dt_real.median().item() / 100:.1f} us (p90 {dt_real.quantile(0.9).item() / 100:.1f}); "
+              f"span {span:.1f} us, sum(wave)/1024 SIMDs {busy:.1f} us", flush=True)
+        torch.save(w, "gpurun_out/stamps.pt")
+        continue
     for k, fn in runs.items():
         fn(); fn()
         torch.cuda.synchronize()

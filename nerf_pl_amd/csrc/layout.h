@@ -51,6 +51,10 @@
 // ReLU masks are bits: word d of a lane covers tiles 2d, 2d+1 (bit 16*(t&1)+r).
 #define NR_BLK 32
 #define NR_NATIVE(w) ((w) * NR_BLK)
+// blocks held by a save / gradient buffer of n samples: padded to whole
+// 4-wave workgroups, so a workgroup's dead waves store into padding instead
+// of branching around their stores (ops.n_blocks)
+__host__ __device__ __forceinline__ int64_t nr_blocks_pad(int64_t n) { return ((n + 127) / 128) * 4; }
 #define NR_MASK_LAYERS 9          // h1..h8, hdir
 #define NR_SAVE_PER_BLOCK (NR_NATIVE(64) + 8 * NR_NATIVE(256) + NR_NATIVE(256) + \
                            NR_NATIVE(128) + NR_NATIVE(32) + NR_MASK_LAYERS * 256)

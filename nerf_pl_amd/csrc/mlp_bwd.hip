@@ -43,8 +43,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
     const int blk = blockIdx.x * kWaves + wave;
-    const int nb = (a.n + 31) / 32;
-    if (blk >= nb) return;                      // no barriers in this kernel
+    const int nb = (int)nr_blocks_pad(a.n);    // segment stride (padded)
+    if (blk >= (a.n + 31) / 32) return;         // no barriers in this kernel
     const int s_raw = blk * 32 + (lane & 31);
     const bool valid = s_raw < a.n;
     const int s = valid ? s_raw : a.n - 1;

@@ -1,11 +1,12 @@
 // Fused MLP backward, data-gradient chain, on bf16x6 split-operand MFMA
 // (autograd of models/nerf.py:83-124; same contract and outputs as
-// mlp_bwd.hip).  Four waves x 32 samples per workgroup carry the gradient
-// backwards through the transposed layers D[in][sample] = W^T[in][out]
-// dz[out][sample]; the transposed weights (packing.BWD3_LAYERS, 136 k-groups
-// of 24 KiB) stream through the LDS ring of x3.h.  ReLU masks are the
-// forward's bit masks, staged in LDS by LDS-DMA; every layer's dz is written
-// block-native for the weight-gradient GEMMs (wgrad.hip).
+// mlp_bwd.hip, activations in x3.h's N16 layout).  Four waves x 32 samples
+// per workgroup carry the gradient backwards through the transposed layers
+// D[in][sample] = W^T[in][out] dz[out][sample] on v_mfma_f32_16x16x32_bf16;
+// the transposed weights (packing.BWD3_LAYERS, 136 k-groups of 24 KiB) stream
+// through the LDS ring of x3.h.  ReLU masks are the forward's bit masks,
+// staged in LDS by LDS-DMA; every layer's dz is written block-native (N16)
+// for the weight-gradient GEMMs (wgrad.hip).
 #include "x3.h"
 
 namespace {
@@ -15,28 +16,54 @@ using namespace x3;
 constexpr int kDirT = 0, kFinalT = 8, kL8T = 24, kL7T = 40, kL6T = 56, kL5T = 72, kL4T = 88,
               kL3T = 104, kL2T = 120, kQ = 136;
 constexpr int kMaskBytes = kWaves * NR_MASK_LAYERS * 64 * 16;
-constexpr int kLdsBytes = kRingBytes + kMaskBytes;
+constexpr int kHeadDma = (NR_H_SIZE * 4 + 1023) / 1024;   // fp32 head block, by LDS-DMA
+constexpr int kLdsBytes = kRingBytes + kMaskBytes + kHeadDma * 1024;
 
 struct BwdTab {
-    __host__ __device__ static constexpr int tiles(int) { return 8; }
-    __host__ __device__ static constexpr int64_t off(int q) { return (int64_t)q * 8 * 3072; }
+    __host__ __device__ static constexpr int64_t off(int q) { return (int64_t)q * kSlotBytes; }
 };
 static_assert(BwdTab::off(kQ) == 3342336, "packed size must match packing.BWD3_BYTES");
 
-template <int NT>
-__device__ __forceinline__ void zero(f32x16 (&acc)[8]) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
-}
+// B units of a gradient input dz (NF feature tiles): with MASK the ReLU mask
+// of the forward activation applied (ReLU backward), and the values stored
+// N16 as they are split (units p = 0, 1 of (k-step s, tile S) complete tile
+// 2s, p = 2, 3 tile 2s+1) for the weight-gradient GEMMs
+template <int NF, bool MASK>
+struct GradU {
+    static constexpr bool kStores = true;
+    const f32x4 (&X)[NF][2];
+    float* dst;
+    uint32_t mw[4];
+    int lane;
+    float pend[2] = {0.f, 0.f};
+    template <typename SC>
+    __device__ __forceinline__ void operator()(SC, int sb, int p, float& x0, float& x1) {
+        constexpr int s = SC::value;
+        const int F = 2 * s + (p >> 1), r = 2 * (p & 1);
+        x0 = acc_b(X, s, sb, 2 * p);
+        x1 = acc_b(X, s, sb, 2 * p + 1);
+        if constexpr (MASK) {
+            x0 = mask_keep(x0, mw, F, sb, r);
+            x1 = mask_keep(x1, mw, F, sb, r + 1);
+        }
+        if ((p & 1) == 0) {
+            pend[0] = x0;
+            pend[1] = x1;
+        } else {
+            store_n16(f32x4{pend[0], pend[1], x0, x1}, F, sb, dst, lane);
+        }
+    }
+};
 
-template <int NT>
-__device__ __forceinline__ void relu_mask(f32x16 (&acc)[8], uint4 m) {
-    const uint32_t w[4] = {m.x, m.y, m.z, m.w};
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = nr_mask_bit(acc[t][r], w[t >> 1], 16 * (t & 1) + r);
-}
+// initial accumulator of d h8: W_sigma^T dsigma (nerf.py:115 sigma head)
+struct SigInit {
+    const float* w; int g; float d0, d1;
+    __device__ __forceinline__ f32x4 operator()(int F, int S) const {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(w + 16 * F + 4 * g);
+        const float d = S ? d1 : d0;
+        return f32x4{v[0] * d, v[1] * d, v[2] * d, v[3] * d};
+    }
+};
 
 struct Bwd3Args {
     const char* packed;        // packing.build_bwd3_map layout
@@ -49,131 +76,144 @@ struct Bwd3Args {
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4;
     const int blk = blockIdx.x * kWaves + wave;
-    const int nb = (a.n + 31) / 32;
-    const bool live = blk < nb;                  // dead waves still feed the ring and barriers
-    const int bk = live ? blk : nb - 1;
-    const int s_raw = bk * 32 + (lane & 31);
-    const bool valid = live && s_raw < a.n;
-    const int s = s_raw < a.n ? s_raw : a.n - 1;
+    const int nreal = (a.n + 31) / 32;
+    const int nb = (int)nr_blocks_pad(a.n);     // segment stride; dead waves write padding
+    const bool live = blk < nreal;
     const char* PB = a.packed;
-    const float* H = a.head;
     const float* SV = a.save;
     float* const GD = a.grad;
 
-    // ReLU mask words (9 layers) by LDS-DMA, issued before the ring so the
-    // ring's counted waits cover them
+    // ReLU mask words (9 layers) and the head block by LDS-DMA, issued before
+    // the ring so the ring's counted waits cover them
     uint4* smask = reinterpret_cast<uint4*>(smem + kRingBytes) + wave * NR_MASK_LAYERS * 64;
     {
         const uint4* gm = reinterpret_cast<const uint4*>(SV + nr_sv_mask(nb)) +
-                          (size_t)bk * NR_MASK_LAYERS * 64 + lane;
+                          (size_t)blk * NR_MASK_LAYERS * 64 + lane;
 #pragma unroll
         for (int l = 0; l < NR_MASK_LAYERS; ++l)
             __builtin_amdgcn_global_load_lds(
                 (const void*)(gm + l * 64),
                 (__attribute__((address_space(3))) void*)(smask + l * 64), 16, 0, 0);
     }
-    prologue<BwdTab, kQ>(PB, smem, wave, lane);
-    const f32x4 go = *reinterpret_cast<const f32x4*>(a.g_out + (size_t)s * 4);
-    const f32x4 yo = *reinterpret_cast<const f32x4*>(a.out + (size_t)s * 4);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // masks (and the prologue) landed
-    const uint4* mask = smask + lane;                   // [layer * 64]
-    Frag f0;                                            // tile-0 fragments of the next k-group
-    enter<BwdTab, 0, kQ>(smem, lane, f0);
-
-    float dzr[3];
+    float* Hs = reinterpret_cast<float*>(smem + kRingBytes + kMaskBytes);
+    {
+        const __amdgpu_buffer_rsrc_t hr =
+            __builtin_amdgcn_make_buffer_rsrc((void*)a.head, 0, NR_H_SIZE * 4, 0x00020000);
+        for (int i = wave; i < kHeadDma; i += kWaves)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                hr, (__attribute__((address_space(3))) void*)(Hs + i * 256), 16, lane * 16, i * 1024, 0, 0);
+    }
+    const Dma dma = make_dma(PB, BwdTab::off(kQ), smem, wave, lane);
+    prologue<BwdTab, kQ>(dma);
+    f32x4 go[2], yo[2];
+    bool valid[2];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) dzr[c] = valid ? go[c] * (1.f - yo[c]) * yo[c] : 0.f;
-    const float dsig = valid ? go[3] : 0.f;
-    if (live && h == 0) {
-        f32x4 v = {dzr[0], dzr[1], dzr[2], dsig};
-        *reinterpret_cast<f32x4*>(GD + nr_gd_dhead(nb) + ((size_t)bk * 32 + (lane & 31)) * 4) = v;
+    for (int S = 0; S < 2; ++S) {
+        const int s_raw = blk * 32 + 16 * S + (lane & 15);
+        valid[S] = s_raw < a.n;
+        const int s = valid[S] ? s_raw : a.n - 1;
+        go[S] = *reinterpret_cast<const f32x4*>(a.g_out + (size_t)s * 4);
+        yo[S] = *reinterpret_cast<const f32x4*>(a.out + (size_t)s * 4);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // masks, head (and the prologue) landed
+    __builtin_amdgcn_s_barrier();                       // head visible to every wave
+    const uint4* mask = smask + lane;                   // [layer * 64]
+    const float* H = Hs;
+    Frag f0;                                            // tile-0 fragments of the next k-group
+    enter<0, kQ>(smem, lane, f0);
+
+    float dzr[2][3], dsig[2];
+#pragma unroll
+    for (int S = 0; S < 2; ++S) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            dzr[S][c] = valid[S] ? go[S][c] * (1.f - yo[S][c]) * yo[S][c] : 0.f;
+        dsig[S] = valid[S] ? go[S][3] : 0.f;
+    }
+    if (live && g < 2) {     // lane group g < 2 writes sample tile S = g
+        const int S = g;
+        f32x4 v = {S ? dzr[1][0] : dzr[0][0], S ? dzr[1][1] : dzr[0][1],
+                   S ? dzr[1][2] : dzr[0][2], S ? dsig[1] : dsig[0]};
+        *reinterpret_cast<f32x4*>(GD + nr_gd_dhead(nb) + ((size_t)blk * 32 + 16 * S + (lane & 15)) * 4) = v;
     }
 
     // d hdir = W_rgb^T dz_rgb, masked by the dir-layer ReLU -> dz_dir (128)
-    f32x16 C[8];
+    f32x4 C[8][2];
     {
         const uint4 mk = mask[8 * 64];
-        const uint32_t mw[2] = {mk.x, mk.y};
+        const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int F = 0; F < 8; ++F) {
+            const int f = 16 * F + 4 * g;
+            const f32x4 w0 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + f);
+            const f32x4 w1 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 128 + f);
+            const f32x4 w2 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 256 + f);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int f = 32 * t + 8 * q + 4 * h;
-                const f32x4 w0 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + f);
-                const f32x4 w1 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 128 + f);
-                const f32x4 w2 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 256 + f);
+            for (int S = 0; S < 2; ++S)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float d = fmaf(w2[e], dzr[2], fmaf(w1[e], dzr[1], w0[e] * dzr[0]));
-                    C[t][4 * q + e] = nr_mask_bit(d, mw[t >> 1], 16 * (t & 1) + 4 * q + e);
+                for (int r = 0; r < 4; ++r) {
+                    const float d = fmaf(w2[r], dzr[S][2], fmaf(w1[r], dzr[S][1], w0[r] * dzr[S][0]));
+                    C[F][S][r] = mask_keep(d, mw, F, S, r);
                 }
-            }
+        }
     }
 
-    f32x16 A[8], B[8];
-    auto dzseg = [&](int l) { return GD + nr_gd_dz(l, nb) + (size_t)bk * NR_NATIVE(256); };
-    auto side8 = [&](const f32x16 (&X)[8], float* dst) {
-        return [&X, dst, lane, live](auto gc) {
-            constexpr int g = decltype(gc)::value;
-            if (!live) return;
-            store_native_piece<8>(X, 2 * g, dst, lane);
-            store_native_piece<8>(X, 2 * g + 1, dst, lane);
-        };
+    Act A, B;
+    Pieces b[2];
+    NoSide none;
+    NoNext nonext;
+    ZeroInit zero;
+    auto dzseg = [&](int l) { return GD + nr_gd_dz(l, nb) + (size_t)blk * NR_NATIVE(256); };
+    auto mwords = [&](int l, uint32_t (&w)[4]) {
+        const uint4 m = mask[l * 64];
+        w[0] = m.x; w[1] = m.y; w[2] = m.z; w[3] = m.w;
     };
-    auto from_acc = [](const f32x16 (&X)[8]) {
-        return [&X](auto gc, float (&x)[8]) { acc_group<decltype(gc)::value>(X, x); };
-    };
+#define NR_GRADU(NAME, X, DZ, ML)                                   \
+    GradU<16, true> NAME{X, dzseg(DZ), {0u, 0u, 0u, 0u}, lane};     \
+    mwords(ML, NAME.mw);
 
     // d feat = W_dir[:, :256]^T dz_dir (xyz_encoding_final has no activation); stores dz_dir
-    zero<8>(A);
+    GradU<8, false> uc{C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_NATIVE(128), {0u, 0u, 0u, 0u}, lane};
+    split_all(uc, b);
+    GradU<16, false> ua{A, dzseg(8), {0u, 0u, 0u, 0u}, lane};     // dfeat
+    segment<BwdTab, kDirT, 4, 2, kQ, true>(dma, lane, A, uc, ua, zero, none, b, f0);
+    // d h8 = W_final^T dfeat + W_sigma^T dsigma; dz8 = d h8 * [h8 > 0]
+    NR_GRADU(u8, B, 7, 7)
     {
-        float* cdst = GD + nr_gd_dzdir(nb) + (size_t)bk * NR_NATIVE(128);
-        auto gb = from_acc(C);
-        auto sd = [&](auto gc) {
-            constexpr int g = decltype(gc)::value;
-            if (!live) return;
-            store_native_piece<4>(reinterpret_cast<const f32x16(&)[4]>(C), 2 * g, cdst, lane);
-            store_native_piece<4>(reinterpret_cast<const f32x16(&)[4]>(C), 2 * g + 1, cdst, lane);
-        };
-        segment<BwdTab, kDirT, 0, 8, 8, kQ>(PB, smem, wave, lane, A, gb, sd, f0);
+        SigInit si{H + NR_H_WSIG, g, dsig[0], dsig[1]};
+        segment<BwdTab, kFinalT, 8, 2, kQ, true>(dma, lane, B, ua, u8, si, none, b, f0);
     }
-    // d h8 = W_final^T dfeat + W_sigma^T dsigma, masked by h8; stores dfeat
+    NR_GRADU(u7, A, 6, 6)
+    segment<BwdTab, kL8T, 8, 2, kQ, true>(dma, lane, A, u8, u7, zero, none, b, f0);
+    NR_GRADU(u6, B, 5, 5)
+    segment<BwdTab, kL7T, 8, 2, kQ, true>(dma, lane, B, u7, u6, zero, none, b, f0);
+    NR_GRADU(u5, A, 4, 4)
+    segment<BwdTab, kL6T, 8, 2, kQ, true>(dma, lane, A, u6, u5, zero, none, b, f0);
+    NR_GRADU(u4, B, 3, 3)   // through the h4 columns of the skip layer
+    segment<BwdTab, kL5T, 8, 2, kQ, true>(dma, lane, B, u5, u4, zero, none, b, f0);
+    NR_GRADU(u3, A, 2, 2)
+    segment<BwdTab, kL4T, 8, 2, kQ, true>(dma, lane, A, u4, u3, zero, none, b, f0);
+    NR_GRADU(u2, B, 1, 1)
+    segment<BwdTab, kL3T, 8, 2, kQ, true>(dma, lane, B, u3, u2, zero, none, b, f0);
+    segment<BwdTab, kL2T, 8, 2, kQ, true>(dma, lane, A, u2, nonext, zero, none, b, f0);
+#undef NR_GRADU
+    {   // dz1 = (W2^T dz2) * [h1 > 0]
+        uint32_t mw[4];
+        mwords(0, mw);
+        float* d1 = dzseg(0);
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+        for (int F = 0; F < 16; ++F)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const f32x4 w = *reinterpret_cast<const f32x4*>(H + NR_H_WSIG + 32 * t + 8 * q + 4 * h);
+            for (int S = 0; S < 2; ++S) {
+                f32x4 v = A[F][S];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) B[t][4 * q + e] = w[e] * dsig;
-        }
-    {
-        const uint4 mk = mask[7 * 64];
-        auto gb = from_acc(A);
-        auto sd = side8(A, dzseg(8));
-        segment<BwdTab, kFinalT, 0, 16, 8, kQ>(PB, smem, wave, lane, B, gb, sd, f0);
-        relu_mask<8>(B, mk);
+                for (int r = 0; r < 4; ++r) v[r] = mask_keep(v[r], mw, F, S, r);
+                store_n16(v, F, S, d1, lane);
+            }
     }
-#define NR_BACK3(DST, SRC, Q0, L)                                              \
-    {                                                                          \
-        const uint4 mk = mask[(L - 1) * 64];                                   \
-        zero<8>(DST);                                                          \
-        auto gb = from_acc(SRC);                                               \
-        auto sd = side8(SRC, dzseg(L));                                        \
-        segment<BwdTab, Q0, 0, 16, 8, kQ>(PB, smem, wave, lane, DST, gb, sd, f0); \
-        relu_mask<8>(DST, mk);                                                 \
-    }
-    NR_BACK3(A, B, kL8T, 7)   // dz7 = (W8^T dz8) * [h7 > 0], stores dz8
-    NR_BACK3(B, A, kL7T, 6)
-    NR_BACK3(A, B, kL6T, 5)
-    NR_BACK3(B, A, kL5T, 4)   // through the h4 columns of the skip layer
-    NR_BACK3(A, B, kL4T, 3)
-    NR_BACK3(B, A, kL3T, 2)
-    NR_BACK3(A, B, kL2T, 1)   // stores dz2, leaves dz1 in A
-#undef NR_BACK3
-    if (live) store_native<8>(A, dzseg(0), lane);
 }
 
 __global__ void pack_x3_kernel(const float* __restrict__ flat, const int32_t* __restrict__ map,

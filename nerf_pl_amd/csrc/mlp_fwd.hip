@@ -128,8 +128,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         __syncthreads();
     }
     const float* H = Hs;
-    const int nb = (a.n + 31) / 32;
-    const bool save = a.save != nullptr && blk < nb;     // whole block, tail lanes included
+    const int nb = (int)nr_blocks_pad(a.n);             // segment stride (padded)
+    const bool save = a.save != nullptr && blk < (a.n + 31) / 32;   // whole block, tail lanes included
     float* const SV = a.save;
 
     // ---- point and direction ------------------------------------------------

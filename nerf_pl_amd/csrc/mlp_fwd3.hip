@@ -2,19 +2,20 @@
 //
 // Same contract and outputs as mlp_fwd.hip (models/nerf.py:21-38, 83-124; the
 // chunked loop of models/rendering.py:141-161), but every layer runs on
-// v_mfma_f32_32x32x16_bf16: each fp32 operand is split exactly into three
+// v_mfma_f32_16x16x32_bf16: each fp32 operand is split exactly into three
 // bf16 pieces (hi + mid + lo, round-to-nearest at each step) and the six
 // piece products of order <= 2^-16 are accumulated in fp32 -- fp32-level
 // accuracy at 16/6 = 2.67x the fp32 MFMA rate (packing.py, "bf16x6").
 //
 // Structure: a workgroup of 4 waves (one per SIMD) evaluates 4 x 32 samples.
-// A wave keeps its activations in registers in transposed form
-// D[feature][sample] (a layer's accumulator registers 8s..8s+7 of tile t are
-// the B fragment of k-group 2t+s of the next layer).  The weights are shared
-// by the 4 waves through an LDS ring of k-groups (16 input features x all
-// output tiles x 3 pieces = 24 KiB), filled by LDS-DMA (global_load_lds
-// dwordx4) kSlots-1 groups ahead; one barrier per group hands a slot over.
-// The B-fragment split costs ~45 VALU ops per k-group, hidden between MFMAs.
+// A wave keeps its activations in registers as x3::Act (features x samples,
+// 16x16 accumulator tiles); k-step s of the next layer reads its B fragment
+// from tiles 2s, 2s+1 of the lane's own registers.  The weights are shared by
+// the 4 waves through an LDS ring of k-groups (32 inputs x 128 outputs x 3
+// pieces = 24 KiB), filled by LDS-DMA (global_load_lds dwordx4) kSlots-1
+// groups ahead; one barrier per group hands a slot over.  The B split of the
+// next k-step and the previous layer's saved-activation stores are spread
+// between the MFMAs of the current k-step.
 #include "x3.h"
 
 namespace {
@@ -22,96 +23,152 @@ namespace {
 using namespace x3;
 
 constexpr int kHeadBytes = NR_H_SIZE * 4;
-constexpr int kLdsBytes = kRingBytes + kHeadBytes;
+constexpr int kHeadDma = (kHeadBytes + 1023) / 1024;   // 1 KiB LDS-DMA instructions for the head
+constexpr int kHeadLds = kHeadDma * 1024;
+constexpr int kPeQ = 12;                          // float4 per lane: xyz PE slots (8), dir PE (4)
+constexpr int kPeBytes = kWaves * kPeQ * 64 * 16;  // each wave's encodings, parked for layer 5 / dir
+constexpr int kLdsBytes = kRingBytes + kHeadLds + kPeBytes;
 
 // ---- the k-group sequence (packing.py FWD3_LAYERS) --------------------------
 constexpr int kL1 = 0, kL2 = 4, kL3 = 20, kL4 = 36, kL5 = 52, kL6 = 72, kL7 = 88, kL8 = 104;
-constexpr int kFinal = 120, kDir = 136, kQAll = 154, kQSigma = 120;
+constexpr int kFinal = 120, kDir = 136, kQAll = 145, kQSigma = 120;
 
 struct FwdTab {
-    __host__ __device__ static constexpr int tiles(int q) { return q >= kDir ? 4 : 8; }
     // byte offset of group q inside the packed buffer (head first)
     __host__ __device__ static constexpr int64_t off(int q) {
-        return (int64_t)kHeadBytes + (q <= kDir ? (int64_t)q * 8 * 3072
-                                                : (int64_t)kDir * 8 * 3072 + (int64_t)(q - kDir) * 4 * 3072);
+        return (int64_t)kHeadBytes + (int64_t)q * kSlotBytes;
     }
 };
 static_assert(FwdTab::off(kQAll) == 3575840, "packed size must match packing.fwd3_offsets()");
 
-template <int NT>
-__device__ __forceinline__ void init_bias(f32x16 (&acc)[8], const float* __restrict__ b, int h) {
+// w . relu(x) for both sample tiles, reduced over the 4 lane groups
+template <bool RELU, int NF>
+__device__ __forceinline__ void head_dot(const f32x4 (&acc)[NF][2], const float* __restrict__ w,
+                                         int g, float (&p)[2]) {
+    p[0] = p[1] = 0.f;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int F = 0; F < NF; ++F) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(w + 16 * F + 4 * g);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(b + 32 * t + 8 * q + 4 * h);
-            acc[t][4 * q + 0] = v[0];
-            acc[t][4 * q + 1] = v[1];
-            acc[t][4 * q + 2] = v[2];
-            acc[t][4 * q + 3] = v[3];
-        }
-}
-
-template <int NT>
-__device__ __forceinline__ void relu(f32x16 (&acc)[8]) {
+        for (int S = 0; S < 2; ++S)
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = acc[t][r] > 0.f ? acc[t][r] : 0.f;
-}
-
-template <int NT>
-__device__ __forceinline__ float head_dot(const f32x16 (&acc)[8], const float* __restrict__ w, int h) {
-    float p = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(w + 32 * t + 8 * q + 4 * h);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) p = fmaf(acc[t][4 * q + e], v[e], p);
-        }
-    return p + __shfl_xor(p, 32);
-}
-
-// positional encoding in the per-lane k-step order of packing.pe_feature
-template <int NP, int KS>
-__device__ __forceinline__ void pe_encode(float (&pe)[KS], float px, float py, float pz, int h) {
-    pe[0] = h ? py : px;
-    pe[1] = h ? 0.f : pz;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-        const int m = i + NP * h;
-        const int k = (m * 11) >> 5;     // m / 3 for m < 32
-        const int c = m - 3 * k;
-        const float v = c == 0 ? px : (c == 1 ? py : pz);
-        const float arg = v * (float)(1 << k);
-        float sn, cs;
-        sincosf(arg, &sn, &cs);
-        pe[2 + i] = sn;
-        pe[2 + NP + i] = cs;
+            for (int r = 0; r < 4; ++r) p[S] = fmaf(RELU ? relu_i(acc[F][S][r]) : acc[F][S][r], v[r], p[S]);
     }
 #pragma unroll
-    for (int g = 2 + 2 * NP; g < KS; ++g) pe[g] = 0.f;
+    for (int S = 0; S < 2; ++S) {
+        p[S] += __shfl_xor(p[S], 16);
+        p[S] += __shfl_xor(p[S], 32);
+    }
 }
 
-template <int NP, int KS>
-__device__ __forceinline__ void pe_gather(float (&pe)[KS], const float* __restrict__ row, int h) {
-    pe[0] = row[h];
-    pe[1] = h ? 0.f : row[2];
+// xyz positional encoding in the slot order of packing.PE16_MAP: lane group g
+// holds slots 32s + 8g + j (s = 0, 1), i.e. cells c = 4s + g of 4 arguments
+// (sin at j = 0..3, cos at j = 4..7); argument m = 4c + i is coordinate m % 3
+// at frequency 2^(m / 3); cell 7 ends with the raw x, y (j = 2, 3) and z (j = 6)
+__device__ __forceinline__ void pe_encode(float (&pe)[16], float px, float py, float pz, int g) {
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-        const int m = i + NP * h;
-        const int k = (m * 11) >> 5;
-        const int c = m - 3 * k;
-        pe[2 + i] = row[3 + 6 * k + c];
-        pe[2 + NP + i] = row[6 + 6 * k + c];
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = 4 * (4 * s + g) + i;
+            const int k = (m * 11) >> 5;     // m / 3 for m < 32
+            const int c = m - 3 * k;
+            const float v = c == 0 ? px : (c == 1 ? py : pz);
+            float sn, cs;
+            sincosf(v * __uint_as_float((uint32_t)(127 + k) << 23), &sn, &cs);
+            pe[8 * s + i] = sn;
+            pe[8 * s + 4 + i] = cs;
+        }
+    if (g == 3) {
+        pe[10] = px; pe[11] = py; pe[14] = pz; pe[15] = 0.f;
     }
-#pragma unroll
-    for (int g = 2 + 2 * NP; g < KS; ++g) pe[g] = 0.f;
 }
+
+__device__ __forceinline__ void pe_gather(float (&pe)[16], const float* __restrict__ row, int g) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = min(4 * (4 * s + g) + i, 29);
+            const int k = (m * 11) >> 5;
+            const int c = m - 3 * k;
+            pe[8 * s + i] = row[3 + 6 * k + c];
+            pe[8 * s + 4 + i] = row[6 + 6 * k + c];
+        }
+    if (g == 3) {
+        pe[10] = row[0]; pe[11] = row[1]; pe[14] = row[2]; pe[15] = 0.f;
+    }
+}
+
+// direction encoding (packing.DIR16_MAP): lane group g = frequency 2^g, sin of
+// the 3 coordinates at j = 0..2, cos at j = 4..6, raw coordinate g at j = 3
+__device__ __forceinline__ void dir_encode(float (&d)[8], float dx, float dy, float dz, int g) {
+    const float sc = __uint_as_float((uint32_t)(127 + g) << 23);
+    sincosf(dx * sc, &d[0], &d[4]);
+    sincosf(dy * sc, &d[1], &d[5]);
+    sincosf(dz * sc, &d[2], &d[6]);
+    d[3] = g == 0 ? dx : (g == 1 ? dy : (g == 2 ? dz : 0.f));
+    d[7] = 0.f;
+}
+
+__device__ __forceinline__ void dir_gather(float (&d)[8], const float* __restrict__ row, int g) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        d[c] = row[3 + 6 * g + c];
+        d[4 + c] = row[6 + 6 * g + c];
+    }
+    d[3] = g < 3 ? row[min(g, 2)] : 0.f;
+    d[7] = 0.f;
+}
+
+// slot values 4u .. 4u+3 (u = 2s + jh of the lane's 8-slot cells) -> the N16
+// saved layout: slots 32s + 8g + 4jh = tile 2s + (g >> 1), group 2(g & 1) + jh
+__device__ __forceinline__ void store_pe4(const float* v, int s, int jh, int S, int g,
+                                          float* __restrict__ blk, int lane) {
+    const int T = 2 * s + (g >> 1), gp = 2 * (g & 1) + jh;
+    *reinterpret_cast<f32x4*>(blk + ((T * 2 + S) * 64 + 16 * gp + (lane & 15)) * 4) =
+        f32x4{v[0], v[1], v[2], v[3]};
+}
+
+struct MaskWords { uint32_t w[4] = {0u, 0u, 0u, 0u}; };
 
 enum FwdMode { FWD_RAYS = 0, FWD_EMB = 1, FWD_PTS = 2 };
+
+// layer 1's side: the xyz PE slots saved N16, 2 float4 per group (tiles 2, 6)
+template <bool SAVE>
+struct PeSide {
+    static constexpr int kBefore7 = SAVE ? 2 : 0;
+    const float (&pe)[2][16];
+    float* dst;
+    int g, lane;
+    template <typename GC>
+    __device__ __forceinline__ void operator()(GC, int t) const {
+        if constexpr (SAVE) {
+            if (t == 2 || t == 6) {
+                const int u = 2 * GC::value + (t == 6), S = u >> 2, s = (u >> 1) & 1, jh = u & 1;
+                store_pe4(&pe[S][8 * s + 4 * jh], s, jh, S, g, dst, lane);
+            }
+        }
+    }
+};
+
+// the dir layer's PE part: the dir PE slots saved N16 at tiles 1, 3, 5, 7
+template <bool SAVE>
+struct DirPeSide {
+    static constexpr int kBefore7 = SAVE ? 3 : 0;
+    const float (&dpe)[2][8];
+    float* dst;
+    int g, lane;
+    template <typename GC>
+    __device__ __forceinline__ void operator()(GC, int t) const {
+        if constexpr (SAVE) {
+            if (t & 1) {
+                const int u = t >> 1;
+                store_pe4(&dpe[u >> 1][4 * (u & 1)], 0, u & 1, u >> 1, g, dst, lane);
+            }
+        }
+    }
+};
 
 struct Fwd3Args {
     const char* packed;  // packing.build_fwd3_map layout: head fp32, then bf16 groups
@@ -120,188 +177,274 @@ struct Fwd3Args {
     float* out; float* save;
 };
 
-template <int MODE, bool SIGMA_ONLY>
+// B units of an accumulator input (x3.h Act): the producer's activation
+// applied (RELU) and, with STORE, the values saved N16 as they are split --
+// units p = 0, 1 of (k-step s, tile S) complete feature tile 2s, p = 2, 3 tile
+// 2s+1 -- with their ReLU bits (MASK); SIG accumulates the sigma head
+// w_sigma . x over the split values (x = h8), so no pass re-reads h8.
+template <bool RELU, bool STORE, bool MASK, bool SIG>
+struct AccU {
+    static constexpr bool kStores = STORE;
+    const f32x4 (&X)[16][2];
+    float* dst;
+    uint32_t* msk;
+    const float* wsig;
+    int lane, g;
+    float pend[2] = {0.f, 0.f};
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    float sig[2] = {0.f, 0.f};
+    template <typename SC>
+    __device__ __forceinline__ void operator()(SC, int sb, int p, float& x0, float& x1) {
+        constexpr int s = SC::value;
+        x0 = acc_b(X, s, sb, 2 * p);
+        x1 = acc_b(X, s, sb, 2 * p + 1);
+        if constexpr (RELU) { x0 = relu_i(x0); x1 = relu_i(x1); }
+        if constexpr (SIG) {
+            // feature kmap16(s, g, 2p) and +1
+            const f32x2 wv = *reinterpret_cast<const f32x2*>(wsig + 32 * s + 16 * (p >> 1) + 4 * g + 2 * (p & 1));
+            sig[sb] = fmaf(x0, wv[0], sig[sb]);
+            sig[sb] = fmaf(x1, wv[1], sig[sb]);
+        }
+        if constexpr (STORE) {
+            if ((p & 1) == 0) {
+                pend[0] = x0;
+                pend[1] = x1;
+            } else {
+                const int F = 2 * s + (p >> 1);
+                const f32x4 v = {pend[0], pend[1], x0, x1};
+                store_n16(v, F, sb, dst, lane);
+                if constexpr (MASK) {
+                    mask_bits(v, F, sb, w);
+                    if (s == 7 && sb == 1 && p == 3)
+                        *reinterpret_cast<uint4*>(msk + lane * 4) = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+        }
+    }
+};
+
+// B units of a positional encoding held per sample tile as [S][8 k + j]
+template <int N>
+struct PeU {
+    static constexpr bool kStores = false;
+    const float (&pe)[2][N];
+    template <typename SC>
+    __device__ __forceinline__ void operator()(SC, int sb, int p, float& x0, float& x1) const {
+        constexpr int s = SC::value;
+        x0 = pe[sb][8 * s + 2 * p];
+        x1 = pe[sb][8 * s + 2 * p + 1];
+    }
+};
+
+template <int MODE, bool SIGMA_ONLY, bool SAVE>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     constexpr bool EMB = MODE == FWD_EMB;
     constexpr int QEND = SIGMA_ONLY ? kQSigma : kQAll;
     __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4;
     const int blk = blockIdx.x * kWaves + wave;
-    const int s_raw = blk * 32 + (lane & 31);
-    const bool valid = s_raw < a.n;
-    const int s = valid ? s_raw : a.n - 1;
-    const char* P = a.packed;
-
-    // head block (biases, sigma/rgb heads) -> LDS, then start the weight ring
-    float* Hs = reinterpret_cast<float*>(smem + kRingBytes);
-    {
-        const f32x4* src = reinterpret_cast<const f32x4*>(P);
-        for (int i = threadIdx.x; i < NR_H_SIZE / 4; i += 64 * kWaves)
-            reinterpret_cast<f32x4*>(Hs)[i] = src[i];
+    int smp[2];
+    bool valid[2];
+#pragma unroll
+    for (int S = 0; S < 2; ++S) {
+        const int s_raw = blk * 32 + 16 * S + (lane & 15);
+        valid[S] = s_raw < a.n;
+        smp[S] = valid[S] ? s_raw : a.n - 1;
     }
-    prologue<FwdTab, QEND>(P, smem, wave, lane);
-    __syncthreads();   // head visible (the DMA stays in flight: waited per group)
-    Frag f0;           // tile-0 fragments of the next k-group
-    enter<FwdTab, 0, QEND>(smem, lane, f0);
+    const char* P = a.packed;
+#if NR_X3_DBG == 8
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+
+    // sample inputs first: they are waited for while the weight DMA below
+    // stays in flight (vmcnt retires in issue order)
+    float pe[2][16], dg[2][8];
+    float in[2][7];
+#pragma unroll
+    for (int S = 0; S < 2; ++S) {
+        const int s = smp[S];
+        if constexpr (EMB) {
+            pe_gather(pe[S], a.x + (size_t)s * a.xstride, g);
+            if constexpr (!SIGMA_ONLY) dir_gather(dg[S], a.x + (size_t)s * a.xstride + NR_XYZ_CH, g);
+        } else if constexpr (MODE == FWD_PTS) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) in[S][c] = a.pts[(size_t)s * 3 + c];
+        } else {
+            const float* r = a.rays + (size_t)(s / a.spr) * 8;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) in[S][c] = r[c];
+            in[S][6] = a.z[s];
+        }
+    }
+
+    // head block (biases, sigma/rgb heads) and the first weight groups by
+    // LDS-DMA; the first ring hand-over waits for both
+    float* Hs = reinterpret_cast<float*>(smem + kRingBytes);
+    const Dma dma = make_dma(P, FwdTab::off(kQAll), smem, wave, lane);
+#pragma unroll
+    for (int i = wave; i < kHeadDma; i += kWaves)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            dma.rsrc, (__attribute__((address_space(3))) void*)(smem + kRingBytes + i * 1024), 16,
+            dma.voff, i * 1024, 0, 0);
+    prologue<FwdTab, QEND>(dma);
     const float* H = Hs;
-    const int nb = (a.n + 31) / 32;
-    const bool save = a.save != nullptr && blk < nb;
+    const int nb = (int)nr_blocks_pad(a.n);
     float* const SV = a.save;
 
-    float px, py, pz, dx = 0.f, dy = 0.f, dz = 0.f;
-    const float* xrow = nullptr;
-    if constexpr (EMB) {
-        xrow = a.x + (size_t)s * a.xstride;
-        px = py = pz = 0.f;
-    } else if constexpr (MODE == FWD_PTS) {
-        px = a.pts[(size_t)s * 3 + 0];
-        py = a.pts[(size_t)s * 3 + 1];
-        pz = a.pts[(size_t)s * 3 + 2];
-    } else {
-        const int ray = s / a.spr;
-        const float* r = a.rays + (size_t)ray * 8;
-        const float zz = a.z[s];
-        px = nr_add(r[0], nr_mul(r[3], zz));   // rendering.py:234, no FMA
-        py = nr_add(r[1], nr_mul(r[4], zz));
-        pz = nr_add(r[2], nr_mul(r[5], zz));
-        dx = r[3]; dy = r[4]; dz = r[5];
+    // PE slots of both sample tiles (and the direction PE): computed once,
+    // parked in LDS for layer 5 and the dir layer
+    f32x4* pe_lds = reinterpret_cast<f32x4*>(smem + kRingBytes + kHeadLds) + wave * kPeQ * 64 + lane;
+#pragma unroll
+    for (int S = 0; S < 2; ++S) {
+        if constexpr (MODE == FWD_PTS) {
+            pe_encode(pe[S], in[S][0], in[S][1], in[S][2], g);
+        } else if constexpr (MODE == FWD_RAYS) {
+            const float zz = in[S][6];
+            pe_encode(pe[S], nr_add(in[S][0], nr_mul(in[S][3], zz)),   // rendering.py:234, no FMA
+                      nr_add(in[S][1], nr_mul(in[S][4], zz)), nr_add(in[S][2], nr_mul(in[S][5], zz)), g);
+            if constexpr (!SIGMA_ONLY) dir_encode(dg[S], in[S][3], in[S][4], in[S][5], g);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        pe_lds[q * 64] = f32x4{pe[q >> 2][4 * (q & 3)], pe[q >> 2][4 * (q & 3) + 1],
+                               pe[q >> 2][4 * (q & 3) + 2], pe[q >> 2][4 * (q & 3) + 3]};
+    if constexpr (!SIGMA_ONLY) {
+#pragma unroll
+        for (int S = 0; S < 2; ++S) {
+            pe_lds[(8 + 2 * S) * 64] = f32x4{dg[S][0], dg[S][1], dg[S][2], dg[S][3]};
+            pe_lds[(9 + 2 * S) * 64] = f32x4{dg[S][4], dg[S][5], dg[S][6], dg[S][7]};
+        }
     }
 
-    f32x16 A[8], B[8];
+    Frag f0;           // tile-0 fragments of the next k-group
+    enter<0, QEND>(smem, lane, f0);
+
+    Act A, B;
+    Pieces b[2];       // pieces of the next k-step
     auto hseg = [&](int l) { return SV + nr_sv_h(l, nb) + (size_t)blk * NR_NATIVE(256); };
     auto mseg = [&](int l) {
         return reinterpret_cast<uint32_t*>(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + l) * 256;
     };
-    // previous layer's 32 output pieces, 2 per k-group, + its ReLU mask
-    auto side_acc = [&](const f32x16 (&X)[8], float* dst, uint32_t* msk) {
-        return [&X, dst, msk, save, lane](auto gc) {
-            constexpr int g = decltype(gc)::value;
-            if (!save) return;
-            store_native_piece<8>(reinterpret_cast<const f32x16(&)[8]>(X), 2 * g, dst, lane);
-            store_native_piece<8>(reinterpret_cast<const f32x16(&)[8]>(X), 2 * g + 1, dst, lane);
-            if (g == 0 && msk) store_mask<8>(reinterpret_cast<const f32x16(&)[8]>(X), msk, lane);
-        };
-    };
-    auto from_acc = [](const f32x16 (&X)[8]) {
-        return [&X](auto gc, float (&x)[8]) { acc_group<decltype(gc)::value>(X, x); };
-    };
     NoSide none;
+    NoNext nonext;
+    ZeroInit zero;
+    auto bias = [&](int off) { return BiasInit{H + off, g}; };
+    using U = AccU<true, SAVE, SAVE, false>;
 
-    {   // layer 1: PE(63) -> 256
-        float pe[NR_PE_KSTEPS];
-        if constexpr (EMB) pe_gather<15, NR_PE_KSTEPS>(pe, xrow, h);
-        else pe_encode<15, NR_PE_KSTEPS>(pe, px, py, pz, h);
-        float* pdst = SV + (size_t)blk * NR_NATIVE(64);
-        init_bias<8>(A, H + NR_H_BIAS(1), h);
-        auto getb = [&](auto gc, float (&x)[8]) {
-            constexpr int g = decltype(gc)::value;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = pe[8 * g + j];
-        };
-        auto side = [&](auto gc) {     // PE values, 2 float4 per group
-            constexpr int g = decltype(gc)::value;
-            if (!save) return;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int grp = 2 * g + u;
-                f32x4 v = {pe[4 * grp], pe[4 * grp + 1], pe[4 * grp + 2], pe[4 * grp + 3]};
-                *reinterpret_cast<f32x4*>(pdst + (grp * 64 + lane) * 4) = v;
-            }
-        };
-        segment<FwdTab, kL1, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, side, f0);
-        relu<8>(A);
+    // layer 1: PE(63) -> 256; stores the PE slots
+    PeU<16> peu{pe};
+    split_all(peu, b);
+    U u1{A, hseg(0), mseg(0), nullptr, lane, g};
+    {
+        PeSide<SAVE> side{pe, SV + (size_t)blk * NR_NATIVE(64), g, lane};
+        auto bi = bias(NR_H_BIAS(1));
+        segment<FwdTab, kL1, 2, 2, QEND, true>(dma, lane, A, peu, u1, bi, side, b, f0);
     }
-#define NR_DENSE3(DST, SRC, Q0, L)                                              \
-    {                                                                           \
-        init_bias<8>(DST, H + NR_H_BIAS(L), h);                                 \
-        auto gb = from_acc(SRC);                                                \
-        auto sd = side_acc(SRC, hseg(L - 2), mseg(L - 2));                      \
-        segment<FwdTab, Q0, 0, 16, 8, QEND>(P, smem, wave, lane, DST, gb, sd, f0);      \
-        relu<8>(DST);                                                           \
-    }
-    NR_DENSE3(B, A, kL2, 2)
-    NR_DENSE3(A, B, kL3, 3)
-    NR_DENSE3(B, A, kL4, 4)
-    {   // layer 5: cat[PE, h4] -> 256 (nerf.py:108-109)
-        float pe[NR_PE_KSTEPS];
-        if constexpr (EMB) pe_gather<15, NR_PE_KSTEPS>(pe, xrow, h);
-        else pe_encode<15, NR_PE_KSTEPS>(pe, px, py, pz, h);
-        init_bias<8>(A, H + NR_H_BIAS(5), h);
-        auto getb = [&](auto gc, float (&x)[8]) {
-            constexpr int g = decltype(gc)::value;
+    U u2{B, hseg(1), mseg(1), nullptr, lane, g};
+    { auto bi = bias(NR_H_BIAS(2)); segment<FwdTab, kL2, 8, 2, QEND, true>(dma, lane, B, u1, u2, bi, none, b, f0); }
+    U u3{A, hseg(2), mseg(2), nullptr, lane, g};
+    { auto bi = bias(NR_H_BIAS(3)); segment<FwdTab, kL3, 8, 2, QEND, true>(dma, lane, A, u2, u3, bi, none, b, f0); }
+    float pe5[2][16];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = pe[8 * g + j];
-        };
-        segment<FwdTab, kL5, 0, 4, 8, QEND>(P, smem, wave, lane, A, getb, none, f0);
-        auto gb = from_acc(B);
-        auto sd = side_acc(B, hseg(3), mseg(3));
-        segment<FwdTab, kL5 + 4, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd, f0);
-        relu<8>(A);
+    for (int q = 0; q < 8; ++q) {
+        const f32x4 v = pe_lds[q * 64];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pe5[q >> 2][4 * (q & 3) + e] = v[e];
     }
-    NR_DENSE3(B, A, kL6, 6)
-    NR_DENSE3(A, B, kL7, 7)
-    NR_DENSE3(B, A, kL8, 8)
-#undef NR_DENSE3
+    PeU<16> pe5u{pe5};
+    { auto bi = bias(NR_H_BIAS(4)); segment<FwdTab, kL4, 8, 2, QEND, true>(dma, lane, B, u3, pe5u, bi, none, b, f0); }
+    // layer 5: cat[PE, h4] -> 256 (nerf.py:108-109)
+    U u4{B, hseg(3), mseg(3), nullptr, lane, g};
+    { auto bi = bias(NR_H_BIAS(5)); segment<FwdTab, kL5, 2, 2, QEND, true>(dma, lane, A, pe5u, u4, bi, none, b, f0); }
+    U u5{A, hseg(4), mseg(4), nullptr, lane, g};
+    segment<FwdTab, kL5 + 4, 8, 2, QEND, false>(dma, lane, A, u4, u5, zero, none, b, f0);
+    U u6{B, hseg(5), mseg(5), nullptr, lane, g};
+    { auto bi = bias(NR_H_BIAS(6)); segment<FwdTab, kL6, 8, 2, QEND, true>(dma, lane, B, u5, u6, bi, none, b, f0); }
+    U u7{A, hseg(6), mseg(6), nullptr, lane, g};
+    { auto bi = bias(NR_H_BIAS(7)); segment<FwdTab, kL7, 8, 2, QEND, true>(dma, lane, A, u6, u7, bi, none, b, f0); }
 
-    const float sigma = head_dot<8>(B, H + NR_H_WSIG, h) + H[NR_H_BSIG];
+    // lane group g < 2 writes sample tile S = g
+    const int Sw = g & 1;
+    const bool wr = g < 2 && valid[Sw];
+    const int sw = smp[Sw];
     if constexpr (SIGMA_ONLY) {
-        if (valid && h == 0) a.out[s] = sigma;
+        { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, nonext, bi, none, b, f0); }
+        float sigma[2];
+        head_dot<true>(B, H + NR_H_WSIG, g, sigma);
+        if (wr) a.out[sw] = (Sw ? sigma[1] : sigma[0]) + H[NR_H_BSIG];
         return;
     } else {
-        {   // xyz_encoding_final: no activation (nerf.py:116); stores h8
-            init_bias<8>(A, H + NR_H_BFINAL, h);
-            auto gb = from_acc(B);
-            auto sd = side_acc(B, hseg(7), mseg(7));
-            segment<FwdTab, kFinal, 0, 16, 8, QEND>(P, smem, wave, lane, A, gb, sd, f0);
-        }
+        // h8 feeds xyz_encoding_final and, while it is split, the sigma head
+        AccU<true, SAVE, SAVE, true> u8{B, hseg(7), mseg(7), H + NR_H_WSIG, lane, g};
+        { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, u8, bi, none, b, f0); }
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
-        float dpe[NR_DIR_KSTEPS];
-        if constexpr (EMB) pe_gather<6, NR_DIR_KSTEPS>(dpe, xrow + NR_XYZ_CH, h);
-        else pe_encode<6, NR_DIR_KSTEPS>(dpe, dx, dy, dz, h);
-        f32x16 C[8];
-        init_bias<4>(C, H + NR_H_BDIR, h);
-        {
-            float* fdst = SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256);
-            auto gb = from_acc(A);
-            auto sd = side_acc(A, fdst, nullptr);
-            segment<FwdTab, kDir, 0, 16, 4, QEND>(P, smem, wave, lane, C, gb, sd, f0);
+        float dpe[2][8];
+#pragma unroll
+        for (int S = 0; S < 2; ++S)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const f32x4 v = pe_lds[(8 + 2 * S + h) * 64];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dpe[S][4 * h + e] = v[e];
+            }
+        PeU<8> dpeu{dpe};
+        // xyz_encoding_final: no activation (nerf.py:116)
+        AccU<false, SAVE, false, false> uf{A, SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256),
+                                           nullptr, nullptr, lane, g};
+        { auto bi = bias(NR_H_BFINAL); segment<FwdTab, kFinal, 8, 2, QEND, true>(dma, lane, A, u8, uf, bi, none, b, f0); }
+        float sigma[2];
+#pragma unroll
+        for (int S = 0; S < 2; ++S) {
+            float p = u8.sig[S];
+            p += __shfl_xor(p, 16);
+            p += __shfl_xor(p, 32);
+            sigma[S] = p + H[NR_H_BSIG];
         }
-        {
-            float* ddst = SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32);
-            auto getb = [&](auto gc, float (&x)[8]) {
-                constexpr int g = decltype(gc)::value;
+        f32x4 C[8][2];
+        { auto bi = bias(NR_H_BDIR); segment<FwdTab, kDir, 8, 1, QEND, true>(dma, lane, C, uf, dpeu, bi, none, b, f0); }
+        {   // PE(dir) part (stores the dir PE slots)
+            DirPeSide<SAVE> side{dpe, SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32), g, lane};
+            segment<FwdTab, kDir + 8, 1, 1, QEND, false>(dma, lane, C, dpeu, nonext, zero, side, b, f0);
+        }
+        float zc[3][2];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) x[j] = dpe[8 * g + j];
-            };
-            auto side = [&](auto gc) {
-                constexpr int g = decltype(gc)::value;
-                if (!save) return;
+        for (int c = 0; c < 3; ++c) head_dot<true>(C, H + NR_H_WRGB + 128 * c, g, zc[c]);
+        if (wr) {
+            f32x4 o;
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int grp = 2 * g + u;
-                    f32x4 v = {dpe[4 * grp], dpe[4 * grp + 1], dpe[4 * grp + 2], dpe[4 * grp + 3]};
-                    *reinterpret_cast<f32x4*>(ddst + (grp * 64 + lane) * 4) = v;
+            for (int c = 0; c < 3; ++c) {
+                const float z = (Sw ? zc[c][1] : zc[c][0]) + H[NR_H_BRGB + c];
+                o[c] = 1.f / (1.f + expf(-z));
+            }
+            o[3] = Sw ? sigma[1] : sigma[0];
+            *reinterpret_cast<f32x4*>(a.out + (size_t)sw * 4) = o;
+        }
+#if NR_X3_DBG == 8
+        if (lane == 0) {
+            uint64_t* st = reinterpret_cast<uint64_t*>(a.save) + (size_t)blk * 4;
+            st[0] = r0;
+            st[1] = __builtin_amdgcn_s_memrealtime();
+            st[2] = __builtin_amdgcn_s_memtime() - t0;
+            st[3] = 0;
+        }
+#endif
+        if constexpr (SAVE) {
+            float* hd = SV + nr_sv_hdir(nb) + (size_t)blk * NR_NATIVE(128);
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int F = 0; F < 8; ++F)
+#pragma unroll
+                for (int S = 0; S < 2; ++S) {
+                    f32x4 v = C[F][S];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = relu_i(v[r]);
+                    store_n16(v, F, S, hd, lane);
+                    mask_bits(v, F, S, w);
                 }
-            };
-            segment<FwdTab, kDir + 16, 0, 2, 4, QEND>(P, smem, wave, lane, C, getb, side, f0);
-        }
-        relu<4>(C);
-        float rgb[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float zc = head_dot<4>(C, H + NR_H_WRGB + 128 * c, h) + H[NR_H_BRGB + c];
-            rgb[c] = 1.f / (1.f + expf(-zc));
-        }
-        if (valid && h == 0) {
-            f32x4 o = {rgb[0], rgb[1], rgb[2], sigma};
-            *reinterpret_cast<f32x4*>(a.out + (size_t)s * 4) = o;
-        }
-        if (save) {
-            store_native<4>(reinterpret_cast<const f32x16(&)[4]>(C),
-                            SV + nr_sv_hdir(nb) + (size_t)blk * NR_NATIVE(128), lane);
-            store_mask<4>(reinterpret_cast<const f32x16(&)[4]>(C), mseg(8), lane);
+            *reinterpret_cast<uint4*>(mseg(8) + lane * 4) = make_uint4(w[0], w[1], w[2], w[3]);
         }
     }
 }
@@ -361,16 +504,21 @@ NR_API int nr_mlp_fwd_x3(const void* packed, const float* rays, const float* z, 
     } else {
         NR_REQUIRE(rays && z && samples_per_ray > 0, "nr_mlp_fwd_x3: rays/z/samples_per_ray");
     }
+    NR_REQUIRE(!(sigma_only && save), "nr_mlp_fwd_x3: sigma_only runs keep no activations");
     Fwd3Args a{reinterpret_cast<const char*>(packed), nullptr, rays, z, x, (int)n,
                samples_per_ray, xstride, out, save};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
     hipStream_t st = (hipStream_t)stream;
+    // NR_X3_DBG 8 builds pass the clock-stamp buffer in save
+    const bool sv = save != nullptr && NR_X3_DBG != 8;
     if (emb) {
-        if (sigma_only) mlp_fwd3_kernel<FWD_EMB, true><<<blocks, 64 * kWaves, 0, st>>>(a);
-        else mlp_fwd3_kernel<FWD_EMB, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+        if (sigma_only) mlp_fwd3_kernel<FWD_EMB, true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else if (sv) mlp_fwd3_kernel<FWD_EMB, false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_fwd3_kernel<FWD_EMB, false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
     } else {
-        if (sigma_only) mlp_fwd3_kernel<FWD_RAYS, true><<<blocks, 64 * kWaves, 0, st>>>(a);
-        else mlp_fwd3_kernel<FWD_RAYS, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+        if (sigma_only) mlp_fwd3_kernel<FWD_RAYS, true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else if (sv) mlp_fwd3_kernel<FWD_RAYS, false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_fwd3_kernel<FWD_RAYS, false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
     }
     NR_LAUNCH_CHECK("nr_mlp_fwd_x3");
     return 0;
@@ -385,7 +533,7 @@ NR_API int nr_mlp_sigma_points_x3(const void* packed, const float* pts, int64_t 
     Fwd3Args a{reinterpret_cast<const char*>(packed), pts, nullptr, nullptr, nullptr, (int)n, 1, 0,
                sigma_out, nullptr};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
-    mlp_fwd3_kernel<FWD_PTS, true><<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
+    mlp_fwd3_kernel<FWD_PTS, true, false><<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
     NR_LAUNCH_CHECK("nr_mlp_sigma_points_x3");
     return 0;
 }

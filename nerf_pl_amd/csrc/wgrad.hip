@@ -77,6 +77,7 @@ struct WgArgs {
     int wg_start[kTasks + 1];
     int nb, n;
     float* slab;
+    bool x3;             // segments in the bf16x6 pipeline's N16 layout (x3.h)
 };
 
 // Staging geometry of one 32-sample block of a segment, all compile time:
@@ -281,14 +282,18 @@ constexpr int kOpnd = 3 * kPlane;                // one operand (3 pieces)
 constexpr int kBufB = 2 * kOpnd;                 // one stage buffer (A + B)
 constexpr int kLds = 2 * kBufB;                  // double buffered: 147,456 B
 
-// column of element e of float4 chunk k at lane half h, and chunks per block
+// The bf16x6 pipeline saves every segment in x3.h's N16 layout: float4 (F,
+// S, lane 16g + j) = columns 16F + 4g .. +3 of sample 16S + j (PE segments:
+// columns = PE slots, packing.PE16_MAP / DIR16_MAP).  A staging chunk k is
+// columns 8k .. 8k+7; half h of it is float4 group g = 2(k & 1) + h of tile
+// F = k >> 1.
 template <int KIND, int W>
 struct Geo3 {
     static constexpr int CHUNKS = KIND == SEG_ACC ? W / 8 : (KIND == SEG_PE ? 8 : (KIND == SEG_DPE ? 4 : 0));
-    __device__ static __forceinline__ int col(int k, int h) {
-        if constexpr (KIND == SEG_ACC) return 32 * (k >> 2) + 8 * (k & 3) + 4 * h;
-        else if constexpr (KIND == SEG_PE) return 32 * h + 4 * k;
-        else return 16 * h + 4 * k;
+    __device__ static __forceinline__ int col(int k, int h) { return 8 * k + 4 * h; }
+    // float4 index inside a block of sample j of half-block hb
+    __device__ static __forceinline__ int f4(int k, int h, int hb, int j) {
+        return ((k >> 1) * 2 + hb) * 64 + 16 * (2 * (k & 1) + h) + j;
     }
 };
 
@@ -311,13 +316,13 @@ struct Stager {
     // samples 16 hb + 2 jp and +1 of block blk (unconditional: keeps the
     // compiler's vmcnt bookkeeping exact across the prefetch)
     __device__ __forceinline__ void load(const float* base, int blk, int hb) {
-        const int j = 16 * hb + 2 * jp;
         if constexpr (KIND == SEG_HEAD) {
-            const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * 32 + j;
+            const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * 32 + 16 * hb + 2 * jp;
             v0 = p[0]; v1 = p[1];
         } else {
             constexpr int F4 = Geo3<KIND, W>::CHUNKS * 64;
-            const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * F4 + k * 64 + 32 * h + j;
+            const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * F4 +
+                             Geo3<KIND, W>::f4(k, h, hb, 2 * jp);
             v0 = p[0]; v1 = p[1];
         }
     }
@@ -529,18 +534,33 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
     }
 }
 
+// Embedding channel of bf16x6 PE slot q (packing._pe16_channel / _dir16_channel)
+__device__ __forceinline__ int pe16_channel(int q) {
+    if (q == 58 || q == 59) return q - 58;
+    if (q == 62) return 2;
+    const int c = q >> 3, j = q & 7, m = 4 * c + (j & 3);
+    if (m >= 30) return -1;
+    return (j < 4 ? 3 : 6) + 6 * (m / 3) + m % 3;
+}
+__device__ __forceinline__ int dir16_channel(int q) {
+    const int g = q >> 3, j = q & 7;
+    if (j == 3) return g < 3 ? g : -1;
+    if (j == 7) return -1;
+    return (j < 4 ? 3 : 6) + 6 * g + (j & 3);
+}
+
 // destination of output element (o, c) of task t in the flat gradient (-1 = none)
-__device__ int wgrad_dest(int t, int o, int c) {
+__device__ int wgrad_dest(int t, int o, int c, bool x3) {
     switch (t) {
-        case 0: { const int f = pe_feature(c & 31, c >> 5, 15);
+        case 0: { const int f = x3 ? pe16_channel(c) : pe_feature(c & 31, c >> 5, 15);
                   return f < 0 ? -1 : kP.w[0] + o * kP.fan[0] + f; }
         case 1: case 2: case 3: return kP.w[t] + o * kP.fan[t] + c;
-        case 4: { const int f = pe_feature(c & 31, c >> 5, 15);
+        case 4: { const int f = x3 ? pe16_channel(c) : pe_feature(c & 31, c >> 5, 15);
                   return f < 0 ? -1 : kP.w[4] + o * kP.fan[4] + f; }
         case 5: return kP.w[4] + o * kP.fan[4] + NR_XYZ_CH + c;
         case 6: case 7: case 8: case 9: return kP.w[t - 1] + o * kP.fan[t - 1] + c;
         case 10: return kP.w[9] + o * kP.fan[9] + c;
-        case 11: { const int f = pe_feature(c & 15, c >> 4, 6);
+        case 11: { const int f = x3 ? dir16_channel(c) : pe_feature(c & 15, c >> 4, 6);
                    return f < 0 ? -1 : kP.w[9] + o * kP.fan[9] + 256 + f; }
         case 12: return o == 3 ? kP.w[10] + c : -1;
         case 13: return o < 3 ? kP.w[11] + o * kP.fan[11] + c : -1;
@@ -567,7 +587,7 @@ __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     const int nw = M * N, sz = nw + M;
     if (e >= sz) return;
-    const int dst = e < nw ? wgrad_dest(T.id, e / N, e % N) : wgrad_bias_dest(T.id, e - nw);
+    const int dst = e < nw ? wgrad_dest(T.id, e / N, e % N, a.x3) : wgrad_bias_dest(T.id, e - nw);
     if (dst < 0) return;
     const float* p = a.slab + T.slab + e;
     float s = 0.f;
@@ -596,16 +616,17 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
         if (e != hipSuccess) { nr_set_error("nr_wgrad: memset failed"); return (int)e; }
         return 0;
     }
-    const int64_t nb = (n + 31) / 32;
+    const int64_t nb = (n + 31) / 32;          // blocks holding samples (the work)
+    const int64_t nbp = nr_blocks_pad(n);      // segment stride of the buffers
     float* SV = const_cast<float*>(save);
     float* GD = const_cast<float*>(grad_ws);
     auto acc = [](float* p, int w) { return WgSeg{p, SEG_ACC, w}; };
-    const WgSeg pe{SV, SEG_PE, 64}, dpe{SV + nr_sv_dirpe(nb), SEG_DPE, 32};
-    const WgSeg head{GD + nr_gd_dhead(nb), SEG_HEAD, 4};
-    auto H = [&](int l) { return acc(SV + nr_sv_h(l, nb), 256); };
-    auto DZ = [&](int l) { return acc(GD + nr_gd_dz(l, nb), 256); };
-    const WgSeg feat = acc(SV + nr_sv_feat(nb), 256), hdir = acc(SV + nr_sv_hdir(nb), 128);
-    const WgSeg dzdir = acc(GD + nr_gd_dzdir(nb), 128);
+    const WgSeg pe{SV, SEG_PE, 64}, dpe{SV + nr_sv_dirpe(nbp), SEG_DPE, 32};
+    const WgSeg head{GD + nr_gd_dhead(nbp), SEG_HEAD, 4};
+    auto H = [&](int l) { return acc(SV + nr_sv_h(l, nbp), 256); };
+    auto DZ = [&](int l) { return acc(GD + nr_gd_dz(l, nbp), 256); };
+    const WgSeg feat = acc(SV + nr_sv_feat(nbp), 256), hdir = acc(SV + nr_sv_hdir(nbp), 128);
+    const WgSeg dzdir = acc(GD + nr_gd_dzdir(nbp), 128);
     // (a, b, wm, wn); task order fixes wgrad_dest / wgrad_bias_dest
     const WgTask tasks[kTasks] = {
         {DZ(0), pe, 8, 1}, {DZ(1), H(0), 2, 4}, {DZ(2), H(1), 2, 4}, {DZ(3), H(2), 2, 4},
@@ -657,6 +678,7 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     a.nb = (int)nb;
     a.n = (int)n;
     a.slab = workspace;
+    a.x3 = x3;
     if (x3) wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else wgrad_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     NR_LAUNCH_CHECK("nr_wgrad");

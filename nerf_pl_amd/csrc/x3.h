@@ -1,19 +1,39 @@
-// bf16x6 split-operand MFMA machinery shared by the fused MLP kernels
-// (mlp_fwd3.hip, mlp_bwd3.hip): the exact three-piece bf16 split, the
-// six-product v_mfma_f32_32x32x16_bf16 step, and the LDS ring of weight
-// k-groups filled by LDS-DMA and handed over with one barrier per group.
+// bf16x6 split-operand MFMA machinery.
 //
-// A weight table TAB describes the k-group sequence of one packed buffer:
-//   TAB::tiles(q)  output tiles (32 rows) of group q (8 or 4)
-//   TAB::off(q)    byte offset of group q; a group is [piece 3][tile][lane 64][8] bf16
+// Fused MLP kernels (mlp_fwd3.hip, mlp_bwd3.hip): v_mfma_f32_16x16x32_bf16 on
+// the exact three-piece bf16 split of both operands, fed by an LDS ring of
+// weight k-groups that LDS-DMA fills kSlots-1 groups ahead, one barrier per
+// group.  16x16x32 sustains ~1.8x the clock of 32x32x16 on random operands
+// (dev/mfma_rate.hip: 88% vs 48-55% of the dense bf16 peak), so the layers
+// are tiled for it.
+//
+// Register layout of a wave (32 samples = two 16-sample tiles S): a width-W
+// activation is Act = f32x4 [W/16 feature tiles F][2]; lane l (g = l >> 4)
+// holds features 16F + 4g + r (r = 0..3) of sample 16S + (l & 15).  k-step s
+// (32 inputs) of the next layer takes B element j of lane group g from
+// acc[2s + (j >> 2)][S][j & 3]: the weights are packed in that k order
+// (packing.kmap16), so no value crosses lanes between layers.
+//
+// A packed k-group is (k-step, half of the outputs): [piece 3][tile 8]
+// [lane 64][8] bf16 = 24 KiB; tile t = output rows 16t .. 16t+15 of the half.
+// A weight table TAB gives TAB::off(q), the byte offset of group q.
+//
+// wgrad.hip's weight-gradient GEMMs use the 32x32x16 helpers at the end.
 #pragma once
 #include <utility>
 #include "layout.h"
 
 // NR_X3_DBG (timing experiments only, never in the shipped build):
-// 1 = no barrier, 2 = no DMA wait and no barrier, 3 = no DMA at all
+// 1 = no barrier, 2 = no DMA wait and no barrier, 3 = no DMA at all,
+// 4 = no MFMA (fragments still read), 5 = no B split between k-steps,
+// 8 = clock stamps (mlp_fwd3.hip writes s_memtime / s_memrealtime deltas)
 #ifndef NR_X3_DBG
 #define NR_X3_DBG 0
+#endif
+// NR_X3_SGB: interleave one MFMA with this many VALU instructions inside a
+// tile (sched_group_barrier); 0 leaves the order to the scheduler
+#ifndef NR_X3_SGB
+#define NR_X3_SGB 1
 #endif
 
 namespace x3 {
@@ -23,71 +43,91 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWaves = 4;
+constexpr int kTiles = 8;                      // output tiles (16 rows) per k-group
 constexpr int kSlots = 4;                      // ring depth in k-groups
-constexpr int kSlotBytes = 3 * 8 * 1024;       // 3 pieces x 8 tiles x 1 KiB
+constexpr int kSlotBytes = 3 * kTiles * 1024;  // 3 pieces x 8 tiles x 1 KiB
 constexpr int kRingBytes = kSlots * kSlotBytes;
+constexpr int kDma = 3 * kTiles / kWaves;      // DMA instructions per wave per group
 
 template <int V> using IC = std::integral_constant<int, V>;
 
-// DMA instructions one wave issues for group q (each moves one 1 KiB fragment)
-template <class TAB>
-__host__ __device__ constexpr int grp_dma(int q) { return TAB::tiles(q) * 3 / kWaves; }
+typedef f32x4 Act[16][2];                      // 256-wide activation of one wave
 
 // vm operations this wave issued after its DMA for group q by the time group
 // q is consumed: the DMA of the kSlots-2 groups after it (stores only add,
 // so the count is a safe lower bound)
-template <class TAB, int Q, int QEND>
+template <int Q, int QEND>
 __host__ __device__ constexpr int wait_count() {
     int n = 0;
     for (int k = Q + 1; k <= Q + kSlots - 2; ++k)
-        if (k < QEND) n += grp_dma<TAB>(k);
+        if (k < QEND) n += kDma;
     return n;
 }
 
 __device__ __forceinline__ char* slot_ptr(char* ring, int q) { return ring + (q % kSlots) * kSlotBytes; }
 
+// LDS-DMA of the packed weights: buffer_load_dwordx4 ... lds with a scalar
+// byte offset (group offset + fragment) and the lane's 16 B in voffset, the
+// LDS destination (M0) scalar: no VALU per DMA instruction
+struct Dma {
+    __amdgpu_buffer_rsrc_t rsrc;
+    char* ring;
+    int wave;   // wave index, provably uniform (readfirstlane)
+    int voff;   // lane * 16
+};
+
+__device__ __forceinline__ Dma make_dma(const char* packed, int64_t bytes, char* ring, int wave,
+                                        int lane) {
+    Dma d;
+    d.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)packed, 0, (int)bytes, 0x00020000);
+    d.ring = ring;
+    d.wave = wave;
+    d.voff = lane * 16;
+    return d;
+}
+
+// DMA instruction k (of kDma) of this wave for group Q: fragment i = wave + 4k
 template <class TAB, int Q, int QEND>
-__device__ __forceinline__ void stage(const char* __restrict__ packed, char* ring, int wave,
-                                      int lane) {
+__device__ __forceinline__ void dma_one(const Dma& d, int k) {
     if constexpr (Q < QEND && NR_X3_DBG != 3) {
-        constexpr int NT = TAB::tiles(Q);
-        const char* src = packed + TAB::off(Q);
-        char* dst = slot_ptr(ring, Q);
-#pragma unroll
-        for (int k = 0; k < NT * 3 / kWaves; ++k) {
-            const int i = wave + kWaves * k;
-            __builtin_amdgcn_global_load_lds(
-                (const void*)(src + i * 1024 + lane * 16),
-                (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
-        }
+        const int i = d.wave + kWaves * k;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            d.rsrc, (__attribute__((address_space(3))) void*)(slot_ptr(d.ring, Q) + i * 1024), 16,
+            d.voff, (int)TAB::off(Q) + i * 1024, 0, 0);
     }
 }
 
-template <class TAB, int QEND>
-__device__ __forceinline__ void prologue(const char* __restrict__ packed, char* ring, int wave,
-                                         int lane) {
-    static_assert(kSlots == 4, "prologue stages kSlots-1 groups");
-    stage<TAB, 0, QEND>(packed, ring, wave, lane);
-    stage<TAB, 1, QEND>(packed, ring, wave, lane);
-    stage<TAB, 2, QEND>(packed, ring, wave, lane);
-}
-// forward declaration order: enter<> is defined below; kernels call
-// enter<TAB, 0, QEND>(ring, lane, f0) once after the prologue.
-
-// group Q may be read once this wave's DMA landed and every wave passed here
 template <class TAB, int Q, int QEND>
+__device__ __forceinline__ void stage(const Dma& d) {
+#pragma unroll
+    for (int k = 0; k < kDma; ++k) dma_one<TAB, Q, QEND>(d, k);
+}
+
+template <class TAB, int QEND>
+__device__ __forceinline__ void prologue(const Dma& d) {
+    static_assert(kSlots == 4, "prologue stages kSlots-1 groups");
+    stage<TAB, 0, QEND>(d);
+    stage<TAB, 1, QEND>(d);
+    stage<TAB, 2, QEND>(d);
+}
+
+// group Q may be read once this wave's DMA landed and every wave passed here.
+// vmcnt retires in issue order (loads, stores and LDS-DMA together), so the
+// EXTRA stores issued after group Q's DMA in the current group are left in
+// flight too; older stores are waited for (they have had a group to land).
+template <int Q, int QEND, int EXTRA = 0>
 __device__ __forceinline__ void ring_enter() {
     if constexpr (NR_X3_DBG < 2)
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(wait_count<TAB, Q, QEND>()) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(wait_count<Q, QEND>() + EXTRA) : "memory");
     if constexpr (NR_X3_DBG == 0) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
 
 // exact 3-way split of fp32 values into bf16 pieces (round-to-nearest).  The
-// conversions are packed (v_cvt_pk_bf16_f32 is nearly free beside MFMAs) but
-// the residual subtractions stay scalar: packed f32 VALU (v_pk_add_f32) costs
-// ~13 cycles per instruction beside MFMAs (MI355X_MICROARCH.md), so the
-// library is built with -fno-slp-vectorize.
+// conversions are packed (v_cvt_pk_bf16_f32) but the residual subtractions
+// stay scalar: packed f32 VALU (v_pk_add_f32) costs ~13 cycles per
+// instruction beside MFMAs (MI355X_MICROARCH.md), so the library is built
+// with -fno-slp-vectorize.
 __device__ __forceinline__ float bf16_as_f32(bf16x2 v, int i) {
     const uint32_t u = __builtin_bit_cast(uint32_t, v);
     return __uint_as_float(i == 0 ? u << 16 : u & 0xffff0000u);
@@ -101,21 +141,265 @@ __device__ __forceinline__ void split2(float x0, float x1, bf16x2& hi, bf16x2& m
 }
 
 struct Pieces { bf16x8 hi, mid, lo; };
-__device__ __forceinline__ Pieces split8(const float (&x)[8]) {
-    Pieces p;
-#pragma unroll
-    for (int i = 0; i < 8; i += 2) {
-        bf16x2 h, m, l;
-        split2(x[i], x[i + 1], h, m, l);
-        p.hi[i] = h[0]; p.hi[i + 1] = h[1];
-        p.mid[i] = m[0]; p.mid[i + 1] = m[1];
-        p.lo[i] = l[0]; p.lo[i + 1] = l[1];
-    }
-    return p;
+
+// elements j = 2p, 2p+1 of a B fragment
+__device__ __forceinline__ void split_pair(float x0, float x1, int p, Pieces& b) {
+    bf16x2 h, m, l;
+    split2(x0, x1, h, m, l);
+    b.hi[2 * p] = h[0]; b.hi[2 * p + 1] = h[1];
+    b.mid[2 * p] = m[0]; b.mid[2 * p + 1] = m[1];
+    b.lo[2 * p] = l[0]; b.lo[2 * p + 1] = l[1];
 }
 
-// acc += A * B with both operands given as pieces: the six products of order
-// <= 2^-16, small terms first
+// pin a value to this point of the instruction stream (the compiler would
+// otherwise sink the next k-step's split down to its first use, after the
+// barrier, where nothing hides it)
+__device__ __forceinline__ void pin(Pieces& p) {
+    asm volatile("" : "+v"(p.hi), "+v"(p.mid), "+v"(p.lo));
+}
+
+// ReLU as an integer max: negative floats (and -0) have the sign bit set
+__device__ __forceinline__ float relu_i(float x) {
+    return __int_as_float(max(__float_as_int(x), 0));
+}
+
+// the three weight pieces of one output tile of a k-group
+struct Frag { bf16x8 p[3]; };
+
+template <int Q>
+__device__ __forceinline__ void rd_frag(char* ring, int lane, int t, Frag& f) {
+    const char* s = slot_ptr(ring, Q) + lane * 16 + t * 1024;
+    f.p[0] = *reinterpret_cast<const bf16x8*>(s);
+    f.p[1] = *reinterpret_cast<const bf16x8*>(s + kTiles * 1024);
+    f.p[2] = *reinterpret_cast<const bf16x8*>(s + 2 * kTiles * 1024);
+}
+
+// hand group Q over (wait + barrier) and read its tile-0 fragments
+template <int Q, int QEND, int EXTRA = 0>
+__device__ __forceinline__ void enter(char* ring, int lane, Frag& f0) {
+    if constexpr (Q < QEND) {
+        ring_enter<Q, QEND, EXTRA>();
+        rd_frag<Q>(ring, lane, 0, f0);
+    }
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// d[S] = c[S] + W * B[S] for both sample tiles: the six products of order
+// <= 2^-16, small terms first, the two accumulators alternating
+__device__ __forceinline__ void x6_pair(const Frag& w, const Pieces (&b)[2], f32x4 c0, f32x4 c1,
+                                        f32x4& d0, f32x4& d1) {
+    if constexpr (NR_X3_DBG == 4) {
+        asm volatile("" ::"v"(w.p[0]), "v"(w.p[1]), "v"(w.p[2]), "v"(b[0].hi), "v"(b[1].lo));
+        d0 = c0; d1 = c1;
+        return;
+    }
+    c0 = mfma16(w.p[2], b[0].hi, c0);  c1 = mfma16(w.p[2], b[1].hi, c1);
+    c0 = mfma16(w.p[0], b[0].lo, c0);  c1 = mfma16(w.p[0], b[1].lo, c1);
+    c0 = mfma16(w.p[1], b[0].mid, c0); c1 = mfma16(w.p[1], b[1].mid, c1);
+    c0 = mfma16(w.p[1], b[0].hi, c0);  c1 = mfma16(w.p[1], b[1].hi, c1);
+    c0 = mfma16(w.p[0], b[0].mid, c0); c1 = mfma16(w.p[0], b[1].mid, c1);
+    d0 = mfma16(w.p[0], b[0].hi, c0);  d1 = mfma16(w.p[0], b[1].hi, c1);
+}
+
+// initial accumulator of the first k-step of a layer
+struct ZeroInit {
+    __device__ __forceinline__ f32x4 operator()(int, int) const { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+};
+struct BiasInit {     // bias[16F + 4g .. +3] (LDS), the same for both sample tiles
+    const float* b; int g;
+    __device__ __forceinline__ f32x4 operator()(int F, int) const {
+        return *reinterpret_cast<const f32x4*>(b + 16 * F + 4 * g);
+    }
+};
+
+// one k-group: acc[F0 + t][S] (+)= W_q[t] * B[S] for the 8 output tiles; with
+// INIT the k-group starts from cinit(F, S) instead of acc.  On entry f0
+// holds tile 0 of group Q; the fragments of tile t+1 are read while tile t
+// multiplies, and the hand-over of group Q+1 (wait, barrier, its tile-0 read)
+// is done before the last tile's MFMAs, so both the barrier and the first LDS
+// latency of the next group hide under MFMAs in flight.  On exit f0 holds
+// tile 0 of group Q+1.  hook(t) runs inside tile t; its VALU work is
+// interleaved with the tile's 12 MFMAs.
+template <class TAB, int Q, int QEND, int F0, bool INIT, int EXTRA, typename CInit, typename Hook, int NF>
+__device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][2],
+                                         const Pieces (&b)[2], CInit& cinit, Hook& hook, Frag& f0) {
+    Frag f[2];
+    f[0] = f0;
+    f32x4 ci[2][2];
+    if constexpr (INIT) { ci[0][0] = cinit(F0, 0); ci[0][1] = cinit(F0, 1); }
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) {
+        if (t + 1 < kTiles) {
+            rd_frag<Q>(ring, lane, t + 1, f[(t + 1) & 1]);
+            if constexpr (INIT) { ci[(t + 1) & 1][0] = cinit(F0 + t + 1, 0); ci[(t + 1) & 1][1] = cinit(F0 + t + 1, 1); }
+        }
+        if (t == kTiles - 1) enter<Q + 1, QEND, EXTRA>(ring, lane, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4& d0 = acc[F0 + t][0];
+        f32x4& d1 = acc[F0 + t][1];
+        if constexpr (INIT) x6_pair(f[t & 1], b, ci[t & 1][0], ci[t & 1][1], d0, d1);
+        else x6_pair(f[t & 1], b, d0, d1, d0, d1);
+        // keep the tile's MFMAs in this tile: MFMA intrinsics have no side
+        // effects, so without an ordered use the instruction selector may
+        // float them anywhere in the (huge) basic block
+        asm volatile("" : "+a"(d0), "+a"(d1));
+        hook(t);
+#if NR_X3_SGB
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, NR_X3_SGB, 0);  // VALU
+        }
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// ---- layer segments ---------------------------------------------------------
+// A segment is KS k-steps of one layer's inputs with NH output halves: group
+// Q0 + NH s + hf multiplies k-step s into output tiles 8hf .. 8hf+7.
+//   getu(IC<s>, S, p, x0, x1): B elements 2p, 2p+1 of k-step s, sample tile S
+//     (the producer's activation applied: bias is already in the values)
+//   nextu: getu of the segment that follows; its k-step 0 is split during
+//     this segment's last k-step, so no layer boundary waits on a split
+//   cinit(F, S): initial accumulator (INIT: the layer's first segment)
+//   side(IC<G>, t): side work at tile t of group G (output stores)
+// The 8 split units (S, p) of the next k-step run one per tile of the last
+// half's group; one DMA instruction of group Q+3 runs per tile 0..5.
+//   Getters declare kStores (a global store per odd unit), sides kBefore7,
+//   the stores they issue in a group before its tile 7 (where the next
+//   group's DMA is waited for).
+struct NoNext {
+    static constexpr bool kStores = false;
+    template <typename T> __device__ __forceinline__ void operator()(T, int, int, float& x0, float& x1) const {
+        x0 = x1 = 0.f;
+    }
+};
+template <typename T> struct IsNoNext { static constexpr bool value = false; };
+template <> struct IsNoNext<NoNext> { static constexpr bool value = true; };
+
+struct NoSide {
+    static constexpr int kBefore7 = 0;
+    template <typename T> __device__ __forceinline__ void operator()(T, int) const {}
+};
+
+template <typename GetU, int s>
+__device__ __forceinline__ void split_unit(GetU& getu, IC<s>, int u, Pieces (&bn)[2]) {
+    if constexpr (NR_X3_DBG == 5) return;
+    const int sb = u >> 2, p = u & 3;
+    float x0, x1;
+    getu(IC<s>(), sb, p, x0, x1);
+    split_pair(x0, x1, p, bn[sb]);
+    pin(bn[sb]);
+}
+
+template <typename GetU>
+__device__ __forceinline__ void split_all(GetU& getu, Pieces (&b)[2]) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int sb = u >> 2, p = u & 3;
+        float x0, x1;
+        getu(IC<0>(), sb, p, x0, x1);
+        split_pair(x0, x1, p, b[sb]);
+    }
+}
+
+// split unit u (= 4 S + p) run at tile t of half HF: NH = 2 spreads the 8
+// units over tiles 3..6 of both halves (the last k-step's units read output
+// tiles 0, 1 of the layer, final after tiles 0, 1 of half 0); NH = 1 runs
+// one per tile
+template <int NH, int HF>
+__host__ __device__ constexpr int unit_at(int t) {
+    if constexpr (NH == 1) return t;
+    else return t >= 3 && t <= 6 ? 4 * HF + t - 3 : -1;
+}
+// stores a storing getter issues before tile 7 of its group (one per odd unit)
+template <int NH, int HF>
+__host__ __device__ constexpr int stores_before7() {
+    int n = 0;
+    for (int t = 0; t < kTiles - 1; ++t)
+        if (unit_at<NH, HF>(t) >= 0 && (unit_at<NH, HF>(t) & 1)) ++n;
+    return n;
+}
+
+template <class TAB, int Q0, int S, int KS, int NH, int QEND, bool INIT, int HF, typename GetU,
+          typename NextU, typename CInit, typename Side, int NF>
+__device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)[NF][2], GetU& getu,
+                                          NextU& nextu, CInit& cinit, Side& side,
+                                          const Pieces (&b)[2], Pieces (&bn)[2], Frag& f0) {
+    if constexpr (HF < NH) {
+        constexpr int Q = Q0 + NH * S + HF;
+        auto hook = [&](int t) {
+            if (t < kDma) dma_one<TAB, Q + kSlots - 1, QEND>(dma, t);
+            const int u = unit_at<NH, HF>(t);
+            if (u >= 0) {
+                if constexpr (S + 1 < KS) split_unit(getu, IC<S + 1>(), u, bn);
+                else if constexpr (!IsNoNext<NextU>::value) split_unit(nextu, IC<0>(), u, bn);
+            }
+            side(IC<NH * S + HF>(), t);
+        };
+        constexpr bool ust = S + 1 < KS ? GetU::kStores : NextU::kStores;
+        constexpr int extra = (ust ? stores_before7<NH, HF>() : 0) + Side::kBefore7;
+        group_mm<TAB, Q, QEND, 8 * HF, INIT && S == 0, extra>(dma.ring, lane, acc, b, cinit, hook, f0);
+        seg_group<TAB, Q0, S, KS, NH, QEND, INIT, HF + 1>(dma, lane, acc, getu, nextu, cinit, side,
+                                                          b, bn, f0);
+    }
+}
+
+template <class TAB, int Q0, int S, int KS, int NH, int QEND, bool INIT, typename GetU,
+          typename NextU, typename CInit, typename Side, int NF>
+__device__ __forceinline__ void seg_from(const Dma& dma, int lane, f32x4 (&acc)[NF][2], GetU& getu,
+                                         NextU& nextu, CInit& cinit, Side& side,
+                                         Pieces (&b)[2], Frag& f0) {
+    if constexpr (S < KS) {
+        Pieces bn[2];
+        seg_group<TAB, Q0, S, KS, NH, QEND, INIT, 0>(dma, lane, acc, getu, nextu, cinit, side, b, bn, f0);
+        b[0] = bn[0];
+        b[1] = bn[1];
+        seg_from<TAB, Q0, S + 1, KS, NH, QEND, INIT>(dma, lane, acc, getu, nextu, cinit, side, b, f0);
+    }
+}
+
+// b: on entry the pieces of this segment's k-step 0, on exit those of the
+// next segment's k-step 0 (split by nextu)
+template <class TAB, int Q0, int KS, int NH, int QEND, bool INIT, typename GetU, typename NextU,
+          typename CInit, typename Side, int NF>
+__device__ __forceinline__ void segment(const Dma& dma, int lane, f32x4 (&acc)[NF][2], GetU& getu,
+                                        NextU& nextu, CInit& cinit, Side& side, Pieces (&b)[2],
+                                        Frag& f0) {
+    seg_from<TAB, Q0, 0, KS, NH, QEND, INIT>(dma, lane, acc, getu, nextu, cinit, side, b, f0);
+}
+
+// B fragment element of k-step s from an accumulator input (packing.kmap16)
+template <int NF>
+__device__ __forceinline__ float acc_b(const f32x4 (&X)[NF][2], int s, int sb, int j) {
+    return X[2 * s + (j >> 2)][sb][j & 3];
+}
+
+// ---- block-native saved layout of the bf16x6 pipeline ("N16") -------------
+// Width-W segment of a 32-sample block: [F = W/16][S 2][lane 64][4] floats,
+// element (F, S, l, r) = feature 16F + 4(l >> 4) + r of sample 16S + (l & 15):
+// one wave store of acc[F][S] moves a contiguous 1 KiB.
+__device__ __forceinline__ void store_n16(const f32x4& v, int F, int S, float* __restrict__ blk,
+                                          int lane) {
+    *reinterpret_cast<f32x4*>(blk + ((F * 2 + S) * 64 + lane) * 4) = v;
+}
+
+// ReLU mask bits of a post-ReLU activation: word F >> 2 of the lane, bit
+// 8 (F & 3) + 4 S + r (VALU only: bits(x) != 0)
+__device__ __forceinline__ void mask_bits(const f32x4& v, int F, int S, uint32_t (&w)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        w[F >> 2] |= min(__float_as_uint(v[r]), 1u) << (8 * (F & 3) + 4 * S + r);
+}
+__device__ __forceinline__ float mask_keep(float x, const uint32_t (&w)[4], int F, int S, int r) {
+    return nr_mask_bit(x, w[F >> 2], 8 * (F & 3) + 4 * S + r);
+}
+
+// ---- 32x32x16 helpers (wgrad.hip) ------------------------------------------
 __device__ __forceinline__ f32x16 mfma_x6(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                           const Pieces& b, f32x16 acc) {
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b.hi, acc, 0, 0, 0);
@@ -127,35 +411,7 @@ __device__ __forceinline__ f32x16 mfma_x6(const bf16x8& ah, const bf16x8& am, co
     return acc;
 }
 
-// pin a value to this point of the instruction stream (the compiler would
-// otherwise sink the next group's split down to its first use, after the
-// barrier, where nothing hides it)
-__device__ __forceinline__ void pin(Pieces& p) {
-    asm volatile("" : "+v"(p.hi), "+v"(p.mid), "+v"(p.lo));
-}
-
-// the three weight pieces of one output tile of a k-group
-struct Frag { bf16x8 p[3]; };
-
-template <int Q, int NT>
-__device__ __forceinline__ void rd_frag(char* ring, int lane, int t, Frag& f) {
-    const char* s = slot_ptr(ring, Q) + lane * 16 + t * 1024;
-    f.p[0] = *reinterpret_cast<const bf16x8*>(s);
-    f.p[1] = *reinterpret_cast<const bf16x8*>(s + NT * 1024);
-    f.p[2] = *reinterpret_cast<const bf16x8*>(s + 2 * NT * 1024);
-}
-
-// hand group Q over (wait + barrier) and read its tile-0 fragments
-template <class TAB, int Q, int QEND>
-__device__ __forceinline__ void enter(char* ring, int lane, Frag& f0) {
-    if constexpr (Q < QEND) {
-        ring_enter<TAB, Q, QEND>();
-        rd_frag<Q, TAB::tiles(Q)>(ring, lane, 0, f0);
-    }
-}
-
 // acc[j] += A * B[j] for NJ accumulators sharing the A pieces, product-major
-// (independent accumulators alternate, so no MFMA waits on its predecessor)
 template <int NJ>
 __device__ __forceinline__ void mfma_x6_multi(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                               const Pieces (&b)[NJ], f32x16* acc) {
@@ -172,79 +428,5 @@ __device__ __forceinline__ void mfma_x6_multi(const bf16x8& ah, const bf16x8& am
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b[j].hi, acc[j], 0, 0, 0);
 }
-
-// one k-group: acc[t] += W_q[t] * B for the NT output tiles.  On entry f0
-// holds tile 0 of group Q; the fragments of tile t+1 are read while tile t
-// multiplies, and the hand-over of group Q+1 (wait, barrier, its tile-0 read)
-// is done before the last tile's MFMAs, so both the barrier and the first LDS
-// latency of the next group hide under MFMAs in flight.  On exit f0 holds
-// tile 0 of group Q+1.  hook(t) runs after tile t's MFMAs are issued.
-template <class TAB, int Q, int NT, int QEND, typename Hook>
-__device__ __forceinline__ void group_mm(char* ring, int lane, f32x16 (&acc)[8], const Pieces& b,
-                                         Hook& hook, Frag& f0) {
-    Frag f[2];
-    f[0] = f0;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        if (t + 1 < NT) rd_frag<Q, NT>(ring, lane, t + 1, f[(t + 1) & 1]);
-        if (t == NT - 1) enter<TAB, Q + 1, QEND>(ring, lane, f0);
-        __builtin_amdgcn_sched_barrier(0);
-        acc[t] = mfma_x6(f[t & 1].p[0], f[t & 1].p[1], f[t & 1].p[2], b, acc[t]);
-        hook(t);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// A layer segment of NG k-groups starting at global group Q0 (compile-time
-// recursion: ring slots, DMA sources and wait counts are constants).
-//   getb(IC<g>, float (&x)[8]): the 8 fp32 B values of local group g
-//   side(IC<g>): output stores of the previous layer, spread over the groups
-// b holds the pieces of group G (split one group ahead, inside group G-1);
-// f0 carries the next group's tile-0 fragments across groups and segments.
-template <class TAB, int Q0, int G, int NG, int NT, int QEND, typename GetB, typename Side>
-__device__ __forceinline__ void segment_from(const char* __restrict__ packed, char* ring, int wave,
-                                             int lane, f32x16 (&acc)[8], GetB& getb, Side& side,
-                                             const Pieces& b, Frag& f0) {
-    if constexpr (G < NG) {
-        constexpr int Q = Q0 + G;
-        Pieces bn = b;
-        auto hook = [&](int t) {
-            if (t == 0) stage<TAB, Q + kSlots - 1, QEND>(packed, ring, wave, lane);
-            if (t == 1) {
-                if constexpr (G + 1 < NG) {
-                    float x[8];
-                    getb(IC<G + 1>(), x);
-                    bn = split8(x);
-                    pin(bn);
-                }
-            }
-            if (t == 2) side(IC<G>());
-        };
-        group_mm<TAB, Q, NT, QEND>(ring, lane, acc, b, hook, f0);
-        segment_from<TAB, Q0, G + 1, NG, NT, QEND>(packed, ring, wave, lane, acc, getb, side, bn,
-                                                   f0);
-    }
-}
-
-template <class TAB, int Q0, int G, int NG, int NT, int QEND, typename GetB, typename Side>
-__device__ __forceinline__ void segment(const char* __restrict__ packed, char* ring, int wave,
-                                        int lane, f32x16 (&acc)[8], GetB& getb, Side& side,
-                                        Frag& f0) {
-    float x[8];
-    getb(IC<0>(), x);
-    const Pieces b = split8(x);
-    segment_from<TAB, Q0, 0, NG, NT, QEND>(packed, ring, wave, lane, acc, getb, side, b, f0);
-}
-
-// B values of k-group g of a 256-wide accumulator input (packing.kmap3)
-template <int g>
-__device__ __forceinline__ void acc_group(const f32x16 (&X)[8], float (&x)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = X[g >> 1][8 * (g & 1) + j];
-}
-
-struct NoSide {
-    template <typename T> __device__ __forceinline__ void operator()(T) const {}
-};
 
 }  // namespace x3

@@ -28,7 +28,9 @@ GRAD_PER_BLOCK = BLK * (9 * 256 + 128 + 4)
 
 
 def n_blocks(n: int) -> int:
-    return (n + BLK - 1) // BLK
+    """Blocks of a save / gradient buffer: padded to whole 4-wave workgroups
+    (csrc/layout.h nr_blocks_pad)."""
+    return (n + 4 * BLK - 1) // (4 * BLK) * 4
 FWD_PACKED = packing.layer_offsets(packing.FWD_LAYERS)[1] + packing.HEAD_SIZE
 BWD_PACKED = packing.layer_offsets(packing.BWD_LAYERS)[1]
 
@@ -234,6 +236,15 @@ def native_to_rows(seg: torch.Tensor, n: int, width: int) -> torch.Tensor:
     nb = n_blocks(n)
     x = seg[: nb * BLK * width].view(nb, width // 32, 4, 2, BLK, 4)
     return x.permute(0, 4, 1, 2, 3, 5).reshape(nb * BLK, width)[:n]
+
+
+def n16_to_rows(seg: torch.Tensor, n: int, width: int) -> torch.Tensor:
+    """Decode an N16 segment of the bf16x6 pipeline (csrc/x3.h) to (n, width)
+    rows: element [block][F][S][lane=16g+j][r] is column 16F+4g+r of sample
+    16S+j (PE segments: columns are PE slots, packing.PE16_MAP / DIR16_MAP)."""
+    nb = n_blocks(n)
+    x = seg[: nb * BLK * width].view(nb, width // 16, 2, 4, 16, 4)
+    return x.permute(0, 2, 4, 1, 3, 5).reshape(nb * BLK, width)[:n]
 
 
 def pe_to_rows(seg: torch.Tensor, n: int, ksteps: int) -> torch.Tensor:

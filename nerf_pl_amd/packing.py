@@ -218,67 +218,115 @@ def build_bwd_map():
     return m
 
 
-# -- bf16x6 split-operand layout (v_mfma_f32_32x32x16_bf16) --------------------
+# -- bf16x6 split-operand layout (v_mfma_f32_16x16x32_bf16) --------------------
 # Each fp32 operand is split exactly into three bf16 pieces x = hi + mid + lo
 # (round-to-nearest at each step) and a product is formed from the six piece
 # products whose order is at most 2^-16 (hi*hi, hi*mid, mid*hi, hi*lo, lo*hi,
 # mid*mid), accumulated in fp32: fp32-level accuracy (the dropped terms are
-# <= 2^-25 relative) at 16/6 = 2.67x the fp32 MFMA rate.
+# <= 2^-25 relative) on the bf16 matrix cores.
 #
-# One k-group = 16 input features.  A 256-wide accumulator input supplies
-# k-group G from tile G>>1, registers 8(G&1)..8(G&1)+7: element j of lane half h
-# is feature kmap3(G, h, j) = 32(G>>1) + 16(G&1) + 8(j>>2) + 4h + (j&3).
-# Positional encodings keep the per-lane k-step order of the fp32 path:
-# element j of k-group G is the lane's pe[8G + j].
+# Register layout of a wave (32 samples = two 16-sample tiles S): an
+# activation of width W is W/16 feature tiles F of 16x16 accumulators; lane l
+# (g = l >> 4) holds rows 4g..4g+3 of every tile for sample 16 S + (l & 15).
+# k-step s of a 256-wide input (32 features) takes, for lane group g, element
+# j of its B fragment from tile 2s + (j >> 2), register j & 3:
+#     kmap16(s, g, j) = 32 s + 16 (j >> 2) + 4 g + (j & 3).
+# Positional encodings: lane group g of k-step s holds the 8 PE "slots"
+# 32 s + 8 g + j, mapped to Embedding channels by PE16_MAP / DIR16_MAP (each
+# lane evaluates sin and cos of the same 4 arguments).
 #
-# Packed group: [piece 3][tile NT][lane 64][j 8] bf16 = NT * 3 KiB, so one
-# ds_read_b128 / global_load_lds_dwordx4 moves one (piece, tile) fragment.
-# Buffer: [head fp32, HEAD_SIZE floats][groups of every layer, in order].
-def kmap3(G, h, j):
-    G, h, j = np.asarray(G), np.asarray(h), np.asarray(j)
-    return 32 * (G >> 1) + 16 * (G & 1) + 8 * (j >> 2) + 4 * h + (j & 3)
+# Packed group = (k-step, half of the outputs): [piece 3][tile 8][lane 64][j 8]
+# bf16 = 24 KiB; tile t covers output rows 128 half + 16 t .. +15 (lane & 15),
+# k = 8 (lane >> 4) + j.  One ds_read_b128 / global_load_lds_dwordx4 moves
+# one (piece, tile) fragment.  Buffer: [head fp32, HEAD_SIZE floats][groups].
+def kmap16(s, g, j):
+    s, g, j = np.asarray(s), np.asarray(g), np.asarray(j)
+    return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3)
 
 
-FWD3_LAYERS = OrderedDict([          # name -> (k-groups, tiles)
-    ("L1", (4, 8)),
-    ("L2", (16, 8)), ("L3", (16, 8)), ("L4", (16, 8)),
-    ("L5", (20, 8)),
-    ("L6", (16, 8)), ("L7", (16, 8)), ("L8", (16, 8)),
-    ("final", (16, 8)),
-    ("dir", (18, 4)),
+def _pe16_channel(slot, n_args, raw):
+    """Embedding channel of PE slot (32 s + 8 g + j) or -1 (pad).  Cell
+    c = slot // 8 holds arguments 4c..4c+3: sin at j = 0..3, cos at j = 4..7;
+    the raw coordinates fill the slots left over after the last argument.
+    raw: slot -> coordinate for the raw x/y/z channels."""
+    if slot in raw:
+        return raw[slot]
+    c, j = divmod(slot, 8)
+    a = 4 * c + (j & 3)
+    if a >= n_args:
+        return -1
+    k, coord = divmod(a, 3)
+    return (3 if j < 4 else 6) + 6 * k + coord
+
+
+# xyz: 30 arguments (10 freqs x 3), slots 58, 59, 62 = raw x, y, z (cell 7:
+# args 28, 29 at j = 0, 1 / 4, 5); dir: 12 arguments, cells 0..3 hold args
+# 3g..3g+2 (j = 0..2 sin, 4..6 cos), raw coordinate g at j = 3.
+PE16_MAP = np.array([_pe16_channel(q, 30, {58: 0, 59: 1, 62: 2}) for q in range(64)])
+
+
+def _dir16_channel(slot):
+    g, j = divmod(slot, 8)
+    if j == 3:
+        return g if g < 3 else -1
+    if j == 7:
+        return -1
+    a = 3 * g + (j & 3)
+    k, coord = divmod(a, 3)
+    return (3 if j < 4 else 6) + 6 * k + coord
+
+
+DIR16_MAP = np.array([_dir16_channel(q) for q in range(32)])
+
+FWD3_LAYERS = OrderedDict([          # name -> (k-steps, output halves)
+    ("L1", (2, 2)),
+    ("L2", (8, 2)), ("L3", (8, 2)), ("L4", (8, 2)),
+    ("L5", (10, 2)),
+    ("L6", (8, 2)), ("L7", (8, 2)), ("L8", (8, 2)),
+    ("final", (8, 2)),
+    ("dir", (9, 1)),
 ])
+GROUP_BYTES = 3 * 8 * 1024
 HEAD_BYTES = HEAD_SIZE * 4
 
 
 def fwd3_offsets():
     """Byte offset of every layer's first group, and the total buffer size."""
     offs, o = OrderedDict(), HEAD_BYTES
-    for k, (ng, nt) in FWD3_LAYERS.items():
+    for k, (ns, nh) in FWD3_LAYERS.items():
         offs[k] = o
-        o += ng * nt * 3 * 1024
+        o += ns * nh * GROUP_BYTES
     return offs, o
 
 
-def _fwd3_layer_map(w_name, segs, ntiles, offs):
-    """int32 per bf16 slot: flat_index * 4 + piece, or -1 (zero)."""
+def _group_coords(n):
+    """(piece, tile, lane, j) of every bf16 slot of n groups, and the group."""
+    e = np.arange(n * 3 * 8 * 512)
+    grp = e // (3 * 8 * 512)
+    rem = e % (3 * 8 * 512)
+    piece = rem // (8 * 512)
+    t = (rem % (8 * 512)) // 512
+    lane = (rem % 512) // 8
+    j = rem % 8
+    return grp, piece, t, lane, j
+
+
+def _fwd3_layer_map(w_name, segs, nhalf, offs):
+    """int32 per bf16 slot: flat_index * 4 + piece, or -1 (zero).  segs:
+    (k-steps, kind, column offset); groups run k-step major, output half minor."""
     w_off, (rows, fan) = offs[w_name]
     parts = []
-    for ngroups, kind, col0 in segs:
-        e = np.arange(ngroups * 3 * ntiles * 512)
-        G = e // (3 * ntiles * 512)
-        rem = e % (3 * ntiles * 512)
-        piece = rem // (ntiles * 512)
-        T = (rem % (ntiles * 512)) // 512
-        lane = (rem % 512) // 8
-        j = rem % 8
-        h = lane >> 5
-        row = 32 * T + (lane & 31)
+    for nks, kind, col0 in segs:
+        grp, piece, t, lane, j = _group_coords(nks * nhalf)
+        s, half = grp // nhalf, grp % nhalf
+        g = lane >> 4
+        row = 128 * half + 16 * t + (lane & 15)
         if kind == "acc":
-            col = kmap3(G, h, j)
+            col = kmap16(s, g, j)
         elif kind == "pe":
-            col = PE_MAP[8 * G + j, h]
+            col = PE16_MAP[32 * s + 8 * g + j]
         else:
-            col = DIR_MAP[8 * G + j, h]
+            col = DIR16_MAP[32 * s + 8 * g + j]
         ok = (col >= 0) & (row < rows)
         parts.append(np.where(ok, (w_off + row * fan + col0 + np.maximum(col, 0)) * 4 + piece, -1))
     return np.concatenate(parts)
@@ -288,53 +336,49 @@ def build_fwd3_map():
     """(group map over every bf16 slot, head map over HEAD_SIZE floats)."""
     offs, _ = param_offsets()
     L = lambda i: f"xyz_encoding_{i}.0.weight"  # noqa: E731
-    parts = [_fwd3_layer_map(L(1), [(4, "pe", 0)], 8, offs)]
+    parts = [_fwd3_layer_map(L(1), [(2, "pe", 0)], 2, offs)]
     for i in (2, 3, 4):
-        parts.append(_fwd3_layer_map(L(i), [(16, "acc", 0)], 8, offs))
-    parts.append(_fwd3_layer_map(L(5), [(4, "pe", 0), (16, "acc", XYZ_CH)], 8, offs))
+        parts.append(_fwd3_layer_map(L(i), [(8, "acc", 0)], 2, offs))
+    parts.append(_fwd3_layer_map(L(5), [(2, "pe", 0), (8, "acc", XYZ_CH)], 2, offs))
     for i in (6, 7, 8):
-        parts.append(_fwd3_layer_map(L(i), [(16, "acc", 0)], 8, offs))
-    parts.append(_fwd3_layer_map("xyz_encoding_final.weight", [(16, "acc", 0)], 8, offs))
-    parts.append(_fwd3_layer_map("dir_encoding.0.weight", [(16, "acc", 0), (2, "dir", W)], 4, offs))
+        parts.append(_fwd3_layer_map(L(i), [(8, "acc", 0)], 2, offs))
+    parts.append(_fwd3_layer_map("xyz_encoding_final.weight", [(8, "acc", 0)], 2, offs))
+    parts.append(_fwd3_layer_map("dir_encoding.0.weight", [(8, "acc", 0), (1, "dir", W)], 1, offs))
     m = np.concatenate(parts).astype(np.int32)
     assert m.size * 2 + HEAD_BYTES == fwd3_offsets()[1]
     return m, _head_map(offs).astype(np.int32)
 
 
-BWD3_LAYERS = OrderedDict([          # transposed layers of the data-gradient chain
-    ("dirT", (8, 8)), ("finalT", (16, 8)),
-    ("L8T", (16, 8)), ("L7T", (16, 8)), ("L6T", (16, 8)), ("L5T", (16, 8)),
-    ("L4T", (16, 8)), ("L3T", (16, 8)), ("L2T", (16, 8)),
+BWD3_LAYERS = OrderedDict([          # transposed layers: (k-steps over outputs, input halves)
+    ("dirT", (4, 2)), ("finalT", (8, 2)),
+    ("L8T", (8, 2)), ("L7T", (8, 2)), ("L6T", (8, 2)), ("L5T", (8, 2)),
+    ("L4T", (8, 2)), ("L3T", (8, 2)), ("L2T", (8, 2)),
 ])
-BWD3_BYTES = sum(ng * nt * 3 * 1024 for ng, nt in BWD3_LAYERS.values())
+BWD3_BYTES = sum(ns * nh * GROUP_BYTES for ns, nh in BWD3_LAYERS.values())
 
 
-def _bwd3_layer_map(w_name, ngroups, col0, offs):
+def _bwd3_layer_map(w_name, nks, col0, offs):
     """Transposed layer: k runs over the forward layer's OUTPUT features
-    (kmap3 order), the 8 tiles over its input columns col0 .. col0+255."""
+    (kmap16 order), the 16 tiles (two halves of 8) over its input columns
+    col0 .. col0+255."""
     w_off, (rows, fan) = offs[w_name]
-    e = np.arange(ngroups * 3 * 8 * 512)
-    G = e // (3 * 8 * 512)
-    rem = e % (3 * 8 * 512)
-    piece = rem // (8 * 512)
-    T = (rem % (8 * 512)) // 512
-    lane = (rem % 512) // 8
-    j = rem % 8
-    k_out = kmap3(G, lane >> 5, j)
-    c_in = col0 + 32 * T + (lane & 31)
+    grp, piece, t, lane, j = _group_coords(nks * 2)
+    s, half = grp // 2, grp % 2
+    k_out = kmap16(s, lane >> 4, j)
+    c_in = col0 + 128 * half + 16 * t + (lane & 15)
     return (w_off + k_out * fan + c_in) * 4 + piece
 
 
 def build_bwd3_map():
     offs, _ = param_offsets()
     L = lambda i: f"xyz_encoding_{i}.0.weight"  # noqa: E731
-    parts = [_bwd3_layer_map("dir_encoding.0.weight", 8, 0, offs),
-             _bwd3_layer_map("xyz_encoding_final.weight", 16, 0, offs)]
+    parts = [_bwd3_layer_map("dir_encoding.0.weight", 4, 0, offs),
+             _bwd3_layer_map("xyz_encoding_final.weight", 8, 0, offs)]
     for i in (8, 7, 6):
-        parts.append(_bwd3_layer_map(L(i), 16, 0, offs))
-    parts.append(_bwd3_layer_map(L(5), 16, XYZ_CH, offs))
+        parts.append(_bwd3_layer_map(L(i), 8, 0, offs))
+    parts.append(_bwd3_layer_map(L(5), 8, XYZ_CH, offs))
     for i in (4, 3, 2):
-        parts.append(_bwd3_layer_map(L(i), 16, 0, offs))
+        parts.append(_bwd3_layer_map(L(i), 8, 0, offs))
     m = np.concatenate(parts).astype(np.int32)
     assert m.size * 2 == BWD3_BYTES
     return m
