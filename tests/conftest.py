@@ -20,9 +20,13 @@ def golden_cases():
     return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz"))
 
 
-def load_golden(name):
-    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+def load_golden_path(path):
+    with np.load(path, allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
+
+
+def load_golden(name):
+    return load_golden_path(os.path.join(GOLDEN, name + ".npz"))
 
 
 def golden_cfg(fx):
