@@ -34,8 +34,9 @@ sys.path.insert(0, REPO)
 
 FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
 BF16_MFMA_PEAK_TF = 16 * FP32_MFMA_PEAK_TF   # dense bf16 MFMA (1/16 ratio, same guide)
-# bf16x6: every fp32 product costs six bf16 MFMA products -> fp32-equivalent ceiling
-X3_PEAK_TF = BF16_MFMA_PEAK_TF / 6
+# split-operand arithmetics: every fp32 product costs six bf16 (bf16x6) or three
+# fp16 (f16x3; dense fp16 = dense bf16 rate) MFMA products -> fp32-equivalent ceiling
+SPLIT_PRODUCTS = {"bf16x6": 6, "f16x3": 3}
 HBM_PEAK_GBS = 8000.0
 # algorithmic FLOP per sample: forward, data-grad, weight-grad
 FLOP_FWD = 1_186_816
@@ -86,11 +87,11 @@ def install_timers(timer):
     from nerf_pl_amd import _lib, ops
 
     def call_tag(name, *a):
-        if name in ("nr_mlp_fwd", "nr_mlp_fwd_x3"):
+        if name in ("nr_mlp_fwd", "nr_mlp_fwd_x3", "nr_mlp_fwd_h3"):
             return ("mlp_fwd_sigma" if a[7] else "mlp_fwd"), int(a[3])
-        if name in ("nr_mlp_bwd", "nr_mlp_bwd_x3"):
+        if name in ("nr_mlp_bwd", "nr_mlp_bwd_x3", "nr_mlp_bwd_h3"):
             return "mlp_bwd_dgrad", int(a[5])
-        if name in ("nr_wgrad", "nr_wgrad_x3"):
+        if name in ("nr_wgrad", "nr_wgrad_x3", "nr_wgrad_h3"):
             return "mlp_wgrad", int(a[2])
         if name == "nr_adam_step":
             return "adam", 0
@@ -233,24 +234,28 @@ def main():
         avg = sum(durs) / len(durs)
         ach = flop[dom] * nmax / (avg * 1e-3) / 1e12
         traffic, tsrc = None, None
+        math = _math()
+        # PMC-measured HBM bytes of this kernel and arithmetic (scripts/traffic.py)
         tf = os.path.join(REPO, "profiles", "r01", "traffic.json")
         if os.path.exists(tf):
-            t = json.load(open(tf)).get(dom)
-            if t and int(t["samples"]) == nmax:
+            tj = json.load(open(tf))
+            t = tj.get(f"{math}/{dom}") or tj.get(dom)
+            if t and int(t["samples"]) == nmax and t.get("arithmetic", math) == math:
                 traffic = round(t["hbm_bytes"] / 1e9, 3)
                 tsrc = f"profiles/r01/traffic.json ({t['method']})"
-        from nerf_pl_amd import ops as _ops
-        x3 = _ops.MATH == "bf16x6"
-        peak = X3_PEAK_TF if x3 else FP32_MFMA_PEAK_TF
+        np_ = SPLIT_PRODUCTS.get(math)
+        peak = BF16_MFMA_PEAK_TF / np_ if np_ else FP32_MFMA_PEAK_TF
+        basis = {
+            "bf16x6": "bf16x6: fp32 FLOPs on v_mfma_f32_16x16x32_bf16, six bf16 products per "
+                      f"fp32 product -> ceiling = dense bf16 peak {BF16_MFMA_PEAK_TF:.0f} / 6",
+            "f16x3": "f16x3: fp32 FLOPs on v_mfma_f32_16x16x32_f16, three fp16 products per "
+                     f"fp32 product -> ceiling = dense fp16 peak {BF16_MFMA_PEAK_TF:.0f} / 3",
+        }.get(math, "fp32: v_mfma_f32_32x32x2_f32 dense peak")
         roof = dict(bound="mfma", kernel=dom, achieved=round(ach, 2), peak=round(peak, 1),
                     unit="TFLOP/s", frac=round(ach / peak, 4), traffic=traffic,
                     traffic_unit="GB per launch", traffic_source=tsrc,
                     samples_per_launch=nmax, avg_launch_ms=round(avg, 4),
-                    flop_per_sample=flop[dom],
-                    peak_basis=("bf16x6: fp32 FLOPs on v_mfma_f32_32x32x16_bf16, six bf16 "
-                                "products per fp32 product -> ceiling = dense bf16 peak "
-                                f"{BF16_MFMA_PEAK_TF:.0f} / 6" if x3 else
-                                "fp32: v_mfma_f32_32x32x2_f32 dense peak"),
+                    flop_per_sample=flop[dom], peak_basis=basis,
                     frac_of_fp32_mfma_peak=round(ach / FP32_MFMA_PEAK_TF, 4))
         d["share_of_step"] = d["total_ms"] / (ms * args.steps)
 
@@ -271,9 +276,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "mlp_arithmetic": ("bf16x6 (fp32 operands split exactly into 3 bf16 pieces, 6 piece "
-                               "products accumulated in fp32; fp32-level accuracy, parity-tested "
-                               "against the reference at 1e-4)") if _math() == "bf16x6" else "fp32",
+            "mlp_arithmetic": {
+                "bf16x6": "bf16x6 (fp32 operands split exactly into 3 bf16 pieces, 6 piece "
+                          "products accumulated in fp32; fp32-level accuracy, parity-tested "
+                          "against the reference at 1e-4)",
+                "f16x3": "f16x3 (fp32 operands split into 2 fp16 pieces, hi*hi + hi*lo + lo*hi "
+                         "accumulated in fp32 with power-of-two range scaling: the 3xTF32 "
+                         "scheme; fp32 inputs/outputs, parity-tested against the reference "
+                         "at 1e-4)",
+            }.get(_math(), "fp32"),
             "data": "synthetic (Blender-lego 400x400, 100-pose camera orbit, rays generated "
                     "on device per batch, random target colours, seeded default-init NeRF "
                     "coarse+fine)",

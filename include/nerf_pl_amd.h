@@ -53,13 +53,13 @@ int nr_embed(const float* x, int64_t n, int n_freqs, float* out, void* stream);
  *   Embedded path (x != NULL): x is (n, xstride) pre-embedded [xyz_emb(63),
  *     dir_emb(27)] or xyz_emb only when sigma_only (NeRF.forward(x) API).
  *   out: (n,4) [rgb, sigma] or (n,1) sigma when sigma_only.
- *   save: NULL for inference, else n*nr_layout_query(3) floats of activations
- *     kept for nr_mlp_bwd / nr_wgrad (training). */
+ *   save: NULL for inference, else nr_blocks_pad(n)*nr_layout_query(3) + 16
+ *     floats of activations kept for nr_mlp_bwd / nr_wgrad (training). */
 int nr_mlp_fwd(const float* packed_fwd, const float* rays, const float* z, int64_t n,
                int samples_per_ray, const float* x, int xstride, int sigma_only, float* out,
                float* save, void* stream);
 
-/* bf16x6 arithmetic (the default): every fp32 operand split exactly into three
+/* bf16x6 arithmetic: every fp32 operand split exactly into three
  * bf16 pieces, the six piece products of order <= 2^-16 accumulated in fp32 on
  * v_mfma_f32_32x32x16_bf16 -- fp32-level accuracy at 2.67x the fp32 MFMA rate.
  * nr_pack_x3 builds its forward weight buffer (nr_fwd3_packed_bytes() bytes:
@@ -81,6 +81,32 @@ int nr_mlp_sigma_points_x3(const void* packed, const float* pts, int64_t n, floa
 int nr_pack_bwd_x3(const float* flat, const int32_t* map, int64_t n, void* out, void* stream);
 int nr_mlp_bwd_x3(const void* packed_bwd, const float* head, const float* out, const float* g_out,
                   const float* save, int64_t n, float* grad_ws, void* stream);
+
+/* f16x3 arithmetic (the default; the 3xTF32 scheme on CDNA4's fp16 matrix
+ * cores): every fp32 operand split into two fp16 pieces (hi + lo, 22 bits),
+ * the three products hi*hi + hi*lo + lo*hi accumulated in fp32 on
+ * v_mfma_f32_16x16x32_f16 / 32x32x16_f16, with exact power-of-two range
+ * scaling (weights x 2^8; gradients per-sample in the data-gradient chain and
+ * per-layer in the weight gradient).  The *_h3 entry points have the contracts
+ * of their *_x3 twins; buffers: forward nr_fwd3_packed_bytes_h3() = 2,388,000
+ * bytes (fp32 head block with the layer biases x 2^8, then fp16 k-groups of
+ * packing.build_fwd3_map(2)), backward 2,228,224 bytes (build_bwd3_map(2)).
+ * A training save buffer (nr_mlp_fwd_h3 with save) carries 16 floats after
+ * the activations (layout.h NR_STATS) that the forward zeroes, nr_mlp_bwd_h3
+ * fills with gradient maxima and nr_wgrad_h3 reads. */
+int64_t nr_fwd3_packed_bytes_h3(void);
+int nr_pack_h3(const float* flat, const int32_t* map, int64_t n, const int32_t* head_map,
+               void* out, void* stream);
+int nr_mlp_fwd_h3(const void* packed, const float* rays, const float* z, int64_t n,
+                  int samples_per_ray, const float* x, int xstride, int sigma_only, float* out,
+                  float* save, void* stream);
+int nr_mlp_sigma_points_h3(const void* packed, const float* pts, int64_t n, float* sigma_out,
+                           void* stream);
+int nr_pack_bwd_h3(const float* flat, const int32_t* map, int64_t n, void* out, void* stream);
+int nr_mlp_bwd_h3(const void* packed_bwd, const float* head, const float* out, const float* g_out,
+                  const float* save, int64_t n, float* grad_ws, void* stream);
+int nr_wgrad_h3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                float* grad_flat, void* stream);
 
 /* Dense sigma query (extract_color_mesh.py:114-137, the marching-cubes grid):
  * sigma_out (n) = NeRF sigma head at points pts (n,3) -- the sigma-only fused

@@ -22,12 +22,67 @@ constexpr int kLdsBytes = kRingBytes + kMaskBytes + kHeadDma * 1024;
 struct BwdTab {
     __host__ __device__ static constexpr int64_t off(int q) { return (int64_t)q * kSlotBytes; }
 };
-static_assert(BwdTab::off(kQ) == 3342336, "packed size must match packing.BWD3_BYTES");
+static_assert(BwdTab::off(kQ) == (NR_F16 ? 2228224 : 3342336),
+              "packed size must match packing.BWD3_BYTES");
+
+// f16x3 gradient scaling.  Column (= sample) scaling commutes with the
+// transposed layer, D = W^T (sigma dz) = sigma (W^T dz), so every sample
+// carries its own power-of-two scale sigma: B values = sigma * true gradient.
+// A layer's accumulator is 2^kWScale * sigma_in * (true output); the getter
+// that splits it renormalises with the max |B| of its producer (the previous
+// layer, complete by then): sigma_out = sigma_in * 2^(kGT - e(max)), so B values
+// stay near 2^kGT whatever the gradient's magnitude, with 2^(15 - kGT) of
+// headroom for one layer's growth (a layer's growth in max-norm is at most
+// max_row sum|W|, 16 at the default init).  Gradient injected into a layer's
+// accumulator (the sigma head's w_sigma dsigma into d h8) enters the
+// renormalisation as a bound (GradU::inj).  Stored gradients are true values.
+constexpr int kGT = 6;
+constexpr int kGLim = 64;      // largest renormalisation step (binades)
+constexpr int kSigLim = 96;    // |log2 sigma| bound
+struct GScale {
+    float ks[2] = {1.f, 1.f};    // accumulator -> B value
+    float kst[2] = {1.f, 1.f};   // accumulator -> true value (stored)
+    float sig[2] = {1.f, 1.f};   // scale of the B values
+    float mx[2] = {0.f, 0.f};    // max |B value| seen by this lane, per sample tile
+};
+
+// max over the 4 lane groups (the features of a sample)
+__device__ __forceinline__ float max_over_groups(float m) {
+    m = fmaxf(m, __shfl_xor(m, 16));
+    return fmaxf(m, __shfl_xor(m, 32));
+}
+
+// renormalise after a producer: see GScale; inj = bound of the values injected
+// into the accumulator, in the producer's B units
+__device__ __forceinline__ void gscale_from(GScale& sc, const GScale& prod, const float (&inj)[2]) {
+#pragma unroll
+    for (int S = 0; S < 2; ++S) {
+        float f = pow2_norm(fmaxf(max_over_groups(prod.mx[S]), inj[S]), kGT, kGLim);
+        // keep sigma in [2^-kSigLim, 2^kSigLim]: gradients so small that they
+        // flush to zero in fp16 must not drive it to infinity (0 * inf = NaN)
+        const int es = (int)((__float_as_uint(prod.sig[S]) >> 23) & 0xff) - 127;
+        const int ef = (int)((__float_as_uint(f) >> 23) & 0xff) - 127;
+        const int en = min(max(es + ef, -kSigLim), kSigLim);
+        f = __uint_as_float((uint32_t)(127 + en - es) << 23);
+        sc.sig[S] = prod.sig[S] * f;
+        sc.ks[S] = f * kWUnscale;
+        sc.kst[S] = kWUnscale / prod.sig[S];
+    }
+}
+
+// max |true gradient| of a segment over the wave -> stats (atomicMax on the bits)
+__device__ __forceinline__ void report_max(float m, float* stats, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned*>(stats), __float_as_uint(m));
+}
 
 // B units of a gradient input dz (NF feature tiles): with MASK the ReLU mask
 // of the forward activation applied (ReLU backward), and the values stored
 // N16 as they are split (units p = 0, 1 of (k-step s, tile S) complete tile
 // 2s, p = 2, 3 tile 2s+1) for the weight-gradient GEMMs
+// f16x3: B values and stored values are scaled per sample (GScale); begin()
+// renormalises from the getter whose B values produced X
 template <int NF, bool MASK>
 struct GradU {
     static constexpr bool kStores = true;
@@ -36,6 +91,12 @@ struct GradU {
     uint32_t mw[4];
     int lane;
     float pend[2] = {0.f, 0.f};
+    GScale sc;
+    float inj[2] = {0.f, 0.f};
+    template <typename P>
+    __device__ __forceinline__ void begin(const P& prod) {
+        if constexpr (NR_F16) gscale_from(sc, prod.sc, inj);
+    }
     template <typename SC>
     __device__ __forceinline__ void operator()(SC, int sb, int p, float& x0, float& x1) {
         constexpr int s = SC::value;
@@ -46,12 +107,25 @@ struct GradU {
             x0 = mask_keep(x0, mw, F, sb, r);
             x1 = mask_keep(x1, mw, F, sb, r + 1);
         }
-        if ((p & 1) == 0) {
-            pend[0] = x0;
-            pend[1] = x1;
-        } else {
-            store_n16(f32x4{pend[0], pend[1], x0, x1}, F, sb, dst, lane);
+        float t0 = x0, t1 = x1;
+        if constexpr (NR_F16) {
+            t0 = x0 * sc.kst[sb];
+            t1 = x1 * sc.kst[sb];
+            x0 *= sc.ks[sb];
+            x1 *= sc.ks[sb];
+            sc.mx[sb] = fmaxf(sc.mx[sb], fmaxf(fabsf(x0), fabsf(x1)));
         }
+        if ((p & 1) == 0) {
+            pend[0] = t0;
+            pend[1] = t1;
+        } else {
+            store_n16(f32x4{pend[0], pend[1], t0, t1}, F, sb, dst, lane);
+        }
+    }
+    // after the last split: the segment's max |true value| -> stats
+    __device__ __forceinline__ void report(float* stats) const {
+        if constexpr (NR_F16)
+            report_max(fmaxf(sc.mx[0] / sc.sig[0], sc.mx[1] / sc.sig[1]), stats, lane);
     }
 };
 
@@ -71,6 +145,7 @@ struct Bwd3Args {
     const float* out; const float* g_out; const float* save;
     int n;
     float* grad;
+    float* stats;    // f16x3: layout.h nr_sv_stats (inside the save buffer)
 };
 
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
@@ -139,6 +214,14 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
                    S ? dzr[1][2] : dzr[0][2], S ? dsig[1] : dsig[0]};
         *reinterpret_cast<f32x4*>(GD + nr_gd_dhead(nb) + ((size_t)blk * 32 + 16 * S + (lane & 15)) * 4) = v;
     }
+    if constexpr (NR_F16) {
+        float m = 0.f;
+#pragma unroll
+        for (int S = 0; S < 2; ++S)
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(dzr[S][0]), fabsf(dzr[S][1])),
+                               fmaxf(fabsf(dzr[S][2]), fabsf(dsig[S]))));
+        report_max(m, a.stats + 10, lane);
+    }
 
     // d hdir = W_rgb^T dz_rgb, masked by the dir-layer ReLU -> dz_dir (128)
     f32x4 C[8][2];
@@ -171,82 +254,142 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         const uint4 m = mask[l * 64];
         w[0] = m.x; w[1] = m.y; w[2] = m.z; w[3] = m.w;
     };
+    float* const ST = a.stats;
 #define NR_GRADU(NAME, X, DZ, ML)                                   \
     GradU<16, true> NAME{X, dzseg(DZ), {0u, 0u, 0u, 0u}, lane};     \
     mwords(ML, NAME.mw);
 
     // d feat = W_dir[:, :256]^T dz_dir (xyz_encoding_final has no activation); stores dz_dir
-    GradU<8, false> uc{C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_NATIVE(128), {0u, 0u, 0u, 0u}, lane};
-    split_all(uc, b);
+    GradU<8, false> uc{C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_NATIVE(128), {0u, 0u, 0u, 0u},
+                       lane};
     GradU<16, false> ua{A, dzseg(8), {0u, 0u, 0u, 0u}, lane};     // dfeat
+    // f16x3: the sigma head injects w_sigma dsigma (|.| <= max|w_sigma| |dsigma|)
+    // into d h8.  The scales of dz_dir's and dfeat's B values are bounded by it
+    // too, so the d h8 accumulator (which inherits dfeat's scale) stays finite
+    // when dsigma dwarfs the rgb gradient (the 1e10 last-sample delta).
+    float inj[2] = {0.f, 0.f};   // max|w_sigma| |dsigma|, true units
+    if constexpr (NR_F16) {
+        float wm = 0.f;
+#pragma unroll
+        for (int F = 0; F < 16; ++F) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(H + NR_H_WSIG + 16 * F + 4 * g);
+            wm = fmaxf(wm, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        }
+        wm = max_over_groups(wm);
+#pragma unroll
+        for (int S = 0; S < 2; ++S) {
+            inj[S] = wm * fabsf(dsig[S]);
+            // dz_dir holds true values: its B scale from its own max (and the injection)
+            float m = 0.f;
+#pragma unroll
+            for (int F = 0; F < 8; ++F)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(C[F][S][r]));
+            const float f = pow2_norm(fmaxf(max_over_groups(m), inj[S]), kGT, kGLim);
+            uc.sc.ks[S] = f;
+            uc.sc.sig[S] = f;
+            ua.inj[S] = inj[S] * f;
+        }
+    }
+    split_all(uc, b);
     segment<BwdTab, kDirT, 4, 2, kQ, true>(dma, lane, A, uc, ua, zero, none, b, f0);
+    uc.report(ST + 9);
     // d h8 = W_final^T dfeat + W_sigma^T dsigma; dz8 = d h8 * [h8 > 0]
     NR_GRADU(u8, B, 7, 7)
+    if constexpr (NR_F16) {
+#pragma unroll
+        for (int S = 0; S < 2; ++S) u8.inj[S] = inj[S] * ua.sc.sig[S];   // in dfeat's B units
+    }
     {
-        SigInit si{H + NR_H_WSIG, g, dsig[0], dsig[1]};
+        // the accumulator carries 2^kWScale sigma(dfeat) (f16x3), so does its C operand
+        const float c0 = (float)(1 << kWScale) * ua.sc.sig[0], c1 = (float)(1 << kWScale) * ua.sc.sig[1];
+        SigInit si{H + NR_H_WSIG, g, NR_F16 ? dsig[0] * c0 : dsig[0], NR_F16 ? dsig[1] * c1 : dsig[1]};
         segment<BwdTab, kFinalT, 8, 2, kQ, true>(dma, lane, B, ua, u8, si, none, b, f0);
     }
+    ua.report(ST + 8);
     NR_GRADU(u7, A, 6, 6)
     segment<BwdTab, kL8T, 8, 2, kQ, true>(dma, lane, A, u8, u7, zero, none, b, f0);
+    u8.report(ST + 7);
     NR_GRADU(u6, B, 5, 5)
     segment<BwdTab, kL7T, 8, 2, kQ, true>(dma, lane, B, u7, u6, zero, none, b, f0);
+    u7.report(ST + 6);
     NR_GRADU(u5, A, 4, 4)
     segment<BwdTab, kL6T, 8, 2, kQ, true>(dma, lane, A, u6, u5, zero, none, b, f0);
+    u6.report(ST + 5);
     NR_GRADU(u4, B, 3, 3)   // through the h4 columns of the skip layer
     segment<BwdTab, kL5T, 8, 2, kQ, true>(dma, lane, B, u5, u4, zero, none, b, f0);
+    u5.report(ST + 4);
     NR_GRADU(u3, A, 2, 2)
     segment<BwdTab, kL4T, 8, 2, kQ, true>(dma, lane, A, u4, u3, zero, none, b, f0);
+    u4.report(ST + 3);
     NR_GRADU(u2, B, 1, 1)
     segment<BwdTab, kL3T, 8, 2, kQ, true>(dma, lane, B, u3, u2, zero, none, b, f0);
+    u3.report(ST + 2);
     segment<BwdTab, kL2T, 8, 2, kQ, true>(dma, lane, A, u2, nonext, zero, none, b, f0);
+    u2.report(ST + 1);
 #undef NR_GRADU
     {   // dz1 = (W2^T dz2) * [h1 > 0]
         uint32_t mw[4];
         mwords(0, mw);
         float* d1 = dzseg(0);
+        float m1 = 0.f;
+        const float k1[2] = {kWUnscale / u2.sc.sig[0], kWUnscale / u2.sc.sig[1]};
 #pragma unroll
         for (int F = 0; F < 16; ++F)
 #pragma unroll
             for (int S = 0; S < 2; ++S) {
                 f32x4 v = A[F][S];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = mask_keep(v[r], mw, F, S, r);
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = mask_keep(v[r], mw, F, S, r);
+                    if constexpr (NR_F16) {
+                        v[r] *= k1[S];
+                        m1 = fmaxf(m1, fabsf(v[r]));
+                    }
+                }
                 store_n16(v, F, S, d1, lane);
             }
+        if constexpr (NR_F16) report_max(m1, ST + 0, lane);
     }
 }
 
 __global__ void pack_x3_kernel(const float* __restrict__ flat, const int32_t* __restrict__ map,
-                               int64_t n, __bf16* __restrict__ out) {
+                               int64_t n, p1* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int32_t m = map[i];
     float v = 0.f;
     if (m >= 0) {
-        const float w = flat[m >> 2];
+        float w = flat[m >> 2];
+        const int piece = m & 3;
+#if NR_F16
+        w *= (float)(1 << kWScale);
+        const float hi = (float)(_Float16)w;
+        v = piece == 0 ? hi : w - hi;
+#else
         const float hi = (float)(__bf16)w;
         const float r1 = w - hi;
         const float mid = (float)(__bf16)r1;
-        const int piece = m & 3;
         v = piece == 0 ? hi : (piece == 1 ? mid : r1 - mid);
+#endif
     }
-    out[i] = (__bf16)v;
+    out[i] = (p1)v;
 }
 
 }  // namespace
 
-NR_API int nr_pack_bwd_x3(const float* flat, const int32_t* map, int64_t n, void* out,
+NR_API int NR_X3_NAME(nr_pack_bwd)(const float* flat, const int32_t* map, int64_t n, void* out,
                           void* stream) {
     NR_REQUIRE(n == BwdTab::off(kQ) / 2, "nr_pack_bwd_x3: map has %lld entries, expected %lld",
                (long long)n, (long long)(BwdTab::off(kQ) / 2));
     NR_REQUIRE(flat && map && out, "nr_pack_bwd_x3: null pointer");
     pack_x3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-        flat, map, n, reinterpret_cast<__bf16*>(out));
+        flat, map, n, reinterpret_cast<p1*>(out));
     NR_LAUNCH_CHECK("nr_pack_bwd_x3");
     return 0;
 }
 
-NR_API int nr_mlp_bwd_x3(const void* packed_bwd, const float* head, const float* out,
+NR_API int NR_X3_NAME(nr_mlp_bwd)(const void* packed_bwd, const float* head, const float* out,
                          const float* g_out, const float* save, int64_t n, float* grad_ws,
                          void* stream) {
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_bwd_x3: n out of range");
@@ -256,7 +399,9 @@ NR_API int nr_mlp_bwd_x3(const void* packed_bwd, const float* head, const float*
     NR_REQUIRE((((uintptr_t)save | (uintptr_t)grad_ws | (uintptr_t)g_out | (uintptr_t)out |
                  (uintptr_t)packed_bwd | (uintptr_t)head) & 15) == 0,
                "nr_mlp_bwd_x3: buffers must be 16-byte aligned");
-    Bwd3Args a{reinterpret_cast<const char*>(packed_bwd), head, out, g_out, save, (int)n, grad_ws};
+    float* stats = const_cast<float*>(save) + nr_sv_stats(nr_blocks_pad(n));
+    Bwd3Args a{reinterpret_cast<const char*>(packed_bwd), head, out, g_out, save, (int)n, grad_ws,
+               stats};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
     mlp_bwd3_kernel<<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
     NR_LAUNCH_CHECK("nr_mlp_bwd_x3");

@@ -39,7 +39,8 @@ struct FwdTab {
         return (int64_t)kHeadBytes + (int64_t)q * kSlotBytes;
     }
 };
-static_assert(FwdTab::off(kQAll) == 3575840, "packed size must match packing.fwd3_offsets()");
+static_assert(FwdTab::off(kQAll) == (NR_F16 ? 2388000 : 3575840),
+              "packed size must match packing.fwd3_offsets()");
 
 // w . relu(x) for both sample tiles, reduced over the 4 lane groups
 template <bool RELU, int NF>
@@ -185,6 +186,7 @@ struct Fwd3Args {
 template <bool RELU, bool STORE, bool MASK, bool SIG>
 struct AccU {
     static constexpr bool kStores = STORE;
+    template <typename P> __device__ __forceinline__ void begin(const P&) {}
     const f32x4 (&X)[16][2];
     float* dst;
     uint32_t* msk;
@@ -199,6 +201,7 @@ struct AccU {
         x0 = acc_b(X, s, sb, 2 * p);
         x1 = acc_b(X, s, sb, 2 * p + 1);
         if constexpr (RELU) { x0 = relu_i(x0); x1 = relu_i(x1); }
+        if constexpr (kWScale != 0) { x0 *= kWUnscale; x1 *= kWUnscale; }   // exact
         if constexpr (SIG) {
             // feature kmap16(s, g, 2p) and +1
             const f32x2 wv = *reinterpret_cast<const f32x2*>(wsig + 32 * s + 16 * (p >> 1) + 4 * g + 2 * (p & 1));
@@ -227,6 +230,7 @@ struct AccU {
 template <int N>
 struct PeU {
     static constexpr bool kStores = false;
+    template <typename P> __device__ __forceinline__ void begin(const P&) {}
     const float (&pe)[2][N];
     template <typename SC>
     __device__ __forceinline__ void operator()(SC, int sb, int p, float& x0, float& x1) const {
@@ -319,6 +323,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         }
     }
 
+    if constexpr (SAVE && NR_F16) {   // gradient statistics of the backward (layout.h)
+        if (blockIdx.x == 0 && threadIdx.x < NR_STATS) SV[nr_sv_stats(nb) + threadIdx.x] = 0.f;
+    }
+
     Frag f0;           // tile-0 fragments of the next k-group
     enter<0, QEND>(smem, lane, f0);
 
@@ -374,7 +382,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, nonext, bi, none, b, f0); }
         float sigma[2];
         head_dot<true>(B, H + NR_H_WSIG, g, sigma);
-        if (wr) a.out[sw] = (Sw ? sigma[1] : sigma[0]) + H[NR_H_BSIG];
+        if (wr) a.out[sw] = (Sw ? sigma[1] : sigma[0]) * kWUnscale + H[NR_H_BSIG];
         return;
     } else {
         // h8 feeds xyz_encoding_final and, while it is split, the sigma head
@@ -416,7 +424,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             f32x4 o;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                const float z = (Sw ? zc[c][1] : zc[c][0]) + H[NR_H_BRGB + c];
+                const float z = (Sw ? zc[c][1] : zc[c][0]) * kWUnscale + H[NR_H_BRGB + c];
                 o[c] = 1.f / (1.f + expf(-z));
             }
             o[3] = Sw ? sigma[1] : sigma[0];
@@ -440,7 +448,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
                 for (int S = 0; S < 2; ++S) {
                     f32x4 v = C[F][S];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = relu_i(v[r]);
+                    for (int r = 0; r < 4; ++r) v[r] = relu_i(v[r]) * kWUnscale;
                     store_n16(v, F, S, hd, lane);
                     mask_bits(v, F, S, w);
                 }
@@ -449,35 +457,47 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     }
 }
 
-// pack: bf16 pieces of the weights (map: flat*4 + piece, -1 = 0) after the
-// fp32 head block (head_map: flat index, -1 = 0)
+// pack: the weight pieces (map: flat*4 + piece, -1 = 0) after the fp32 head
+// block (head_map: flat index, -1 = 0).  f16x3: weights and the layer biases
+// (the MFMA C operand, head entries before NR_H_WSIG) carry 2^kWScale.
+__device__ __forceinline__ float weight_piece(float w, int piece) {
+#if NR_F16
+    w *= (float)(1 << kWScale);
+    const float hi = (float)(_Float16)w;
+    return piece == 0 ? hi : w - hi;
+#else
+    const float hi = (float)(__bf16)w;
+    const float r1 = w - hi;
+    const float mid = (float)(__bf16)r1;
+    return piece == 0 ? hi : (piece == 1 ? mid : r1 - mid);
+#endif
+}
+
 __global__ void pack3_kernel(const float* __restrict__ flat, const int32_t* __restrict__ map,
                              int64_t n, const int32_t* __restrict__ head_map,
                              char* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < NR_H_SIZE) {
         const int32_t m = head_map[i];
-        reinterpret_cast<float*>(out)[i] = m >= 0 ? flat[m] : 0.f;
+        const float sc = i < NR_H_WSIG ? (float)(1 << kWScale) : 1.f;
+        reinterpret_cast<float*>(out)[i] = m >= 0 ? flat[m] * sc : 0.f;
     }
     if (i >= n) return;
     const int32_t m = map[i];
-    float v = 0.f;
-    if (m >= 0) {
-        const float w = flat[m >> 2];
-        const int piece = m & 3;
-        const float hi = (float)(__bf16)w;
-        const float r1 = w - hi;
-        const float mid = (float)(__bf16)r1;
-        v = piece == 0 ? hi : (piece == 1 ? mid : r1 - mid);
-    }
-    reinterpret_cast<__bf16*>(out + kHeadBytes)[i] = (__bf16)v;
+    const float v = m >= 0 ? weight_piece(flat[m >> 2], m & 3) : 0.f;
+    reinterpret_cast<p1*>(out + kHeadBytes)[i] = (p1)v;
 }
 
 }  // namespace
 
-NR_API int64_t nr_fwd3_packed_bytes(void) { return FwdTab::off(kQAll); }
+#if NR_F16
+#define NR_FWD3_BYTES_NAME nr_fwd3_packed_bytes_h3
+#else
+#define NR_FWD3_BYTES_NAME nr_fwd3_packed_bytes
+#endif
+NR_API int64_t NR_FWD3_BYTES_NAME(void) { return FwdTab::off(kQAll); }
 
-NR_API int nr_pack_x3(const float* flat, const int32_t* map, int64_t n, const int32_t* head_map,
+NR_API int NR_X3_NAME(nr_pack)(const float* flat, const int32_t* map, int64_t n, const int32_t* head_map,
                       void* out, void* stream) {
     NR_REQUIRE(n == (FwdTab::off(kQAll) - kHeadBytes) / 2, "nr_pack_x3: map has %lld entries, "
                "expected %lld", (long long)n, (long long)((FwdTab::off(kQAll) - kHeadBytes) / 2));
@@ -488,7 +508,7 @@ NR_API int nr_pack_x3(const float* flat, const int32_t* map, int64_t n, const in
     return 0;
 }
 
-NR_API int nr_mlp_fwd_x3(const void* packed, const float* rays, const float* z, int64_t n,
+NR_API int NR_X3_NAME(nr_mlp_fwd)(const void* packed, const float* rays, const float* z, int64_t n,
                          int samples_per_ray, const float* x, int xstride, int sigma_only,
                          float* out, float* save, void* stream) {
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_fwd_x3: n=%lld out of range", (long long)n);
@@ -524,7 +544,7 @@ NR_API int nr_mlp_fwd_x3(const void* packed, const float* rays, const float* z, 
     return 0;
 }
 
-NR_API int nr_mlp_sigma_points_x3(const void* packed, const float* pts, int64_t n,
+NR_API int NR_X3_NAME(nr_mlp_sigma_points)(const void* packed, const float* pts, int64_t n,
                                   float* sigma_out, void* stream) {
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_sigma_points_x3: n out of range");
     if (n == 0) return 0;

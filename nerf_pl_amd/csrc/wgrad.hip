@@ -25,7 +25,7 @@ constexpr int kThreads = 512;    // 8 waves: two per SIMD, so one wave's staging
                                  // barrier time overlaps its partner's MFMAs
 constexpr int kCol = 36;         // LDS column stride (floats): [column][32 samples + 4 pad]
 constexpr int kBufA = 256 * kCol;  // one operand region
-constexpr int kBuf = 2 * kBufA;    // one buffer = A + B regions
+[[maybe_unused]] constexpr int kBuf = 2 * kBufA;    // one buffer = A + B regions
 
 enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
 
@@ -70,6 +70,7 @@ struct WgTask {
     int G;               // workgroups
     int64_t slab;        // slab offset (floats) of workgroup 0
     int id;              // task id: selects the gradient destination and the kernel shape
+    int stat;            // f16x3: stats slot of the gradient operand (layout.h NR_STATS)
 };
 
 struct WgArgs {
@@ -78,8 +79,25 @@ struct WgArgs {
     int nb, n;
     float* slab;
     bool x3;             // segments in the bf16x6 pipeline's N16 layout (x3.h)
+    const float* stats;  // f16x3: max |gradient| per segment (mlp_bwd3.hip), else null
 };
 
+// f16x3: the gradient operand of a task is scaled by 2^(kWT - e(max |dz|)) so
+// its largest element sits in [2^kWT, 2^(kWT+1)) < 65504; the input operand
+// (activations, |x| < 65504) is split unscaled.  The reduction divides the
+// weight part of the slab sums by the same power of two (bias sums come from
+// the unscaled values).
+__device__ __forceinline__ float task_scale(const WgArgs& a, const WgTask& T) {
+#if NR_F16
+    constexpr int kWT = 14;
+    return x3::pow2_norm(a.stats[T.stat], kWT, 100);
+#else
+    (void)a; (void)T;
+    return 1.f;
+#endif
+}
+
+#if !NR_F16   // the fp32-MFMA kernel lives in the bf16x6 object only
 // Staging geometry of one 32-sample block of a segment, all compile time:
 // float4 e = tid + 512*i lands at LDS [sample j][column c].  In the
 // block-native order float4 e is (t = e>>8, q = (e>>6)&3, lane = e&63).
@@ -256,6 +274,8 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     }
 }
 
+#endif  // !NR_F16
+
 // ---------------------------------------------------------------------------
 // bf16x6 variant: the same task list and slabs on v_mfma_f32_32x32x16_bf16.
 // A stage is 16 samples (half a block): each thread loads the float4s of two
@@ -276,11 +296,11 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
 #define NR_W3_MULTI 1
 #endif
 namespace w3 {
-constexpr int kColB = 48;                        // bytes per column (16 bf16 + pad)
+constexpr int kColB = 48;                        // bytes per column (16 pieces + pad)
 constexpr int kPlane = 256 * kColB;              // one piece of one operand
-constexpr int kOpnd = 3 * kPlane;                // one operand (3 pieces)
+constexpr int kOpnd = x3::kNP * kPlane;          // one operand (all pieces)
 constexpr int kBufB = 2 * kOpnd;                 // one stage buffer (A + B)
-constexpr int kLds = 2 * kBufB;                  // double buffered: 147,456 B
+constexpr int kLds = 2 * kBufB;                  // double buffered: 147,456 B (bf16x6)
 
 // The bf16x6 pipeline saves every segment in x3.h's N16 layout: float4 (F,
 // S, lane 16g + j) = columns 16F + 4g .. +3 of sample 16S + j (PE segments:
@@ -326,20 +346,20 @@ struct Stager {
             v0 = p[0]; v1 = p[1];
         }
     }
-    // split + store column e of this thread's chunk into an operand image;
-    // samples >= nval become 0; adds the two samples' sum (bias) to s
-    __device__ __forceinline__ void store_e(char* img, int nval, int e, float& s) {
+    // split + store column e of this thread's chunk into an operand image
+    // (values times sc, a power of two); samples >= nval become 0; adds the two
+    // samples' unscaled sum (bias) to s
+    __device__ __forceinline__ void store_e(char* img, int nval, int e, float& s, float sc) {
         if (!ALL && !act) return;
         const int j = 2 * jp;
         const float x0 = j < nval ? v0[e] : 0.f, x1 = j + 1 < nval ? v1[e] : 0.f;
         const int c0 = KIND == SEG_HEAD ? 0 : Geo3<KIND, W>::col(k, h);
         s += x0 + x1;
-        x3::bf16x2 hi, mid, lo;
-        x3::split2(x0, x1, hi, mid, lo);
+        x3::p2 pc[x3::kNP];
+        x3::split_p2(x0 * sc, x1 * sc, pc);
         char* q = img + (c0 + e) * kColB + 4 * jp;
-        *reinterpret_cast<x3::bf16x2*>(q) = hi;
-        *reinterpret_cast<x3::bf16x2*>(q + kPlane) = mid;
-        *reinterpret_cast<x3::bf16x2*>(q + 2 * kPlane) = lo;
+#pragma unroll
+        for (int i = 0; i < x3::kNP; ++i) *reinterpret_cast<x3::p2*>(q + i * kPlane) = pc[i];
     }
 };
 }  // namespace w3
@@ -386,13 +406,14 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
         sa[set].load(T.a.base, blk, hb);
         sb[set].load(T.b.base, blk, hb);
     };
+    const float sca = task_scale(a, T);
     auto store = [&](int set, int buf, int st) {
         const int nval = st < nst ? a.n - (b0 + (st >> 1)) * 32 - 16 * (st & 1) : 0;
         float sdummy = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            sa[set].store_e(lds + buf * kBufB, nval, e, bacc[e]);
-            sb[set].store_e(lds + buf * kBufB + kOpnd, nval, e, sdummy);
+            sa[set].store_e(lds + buf * kBufB, nval, e, bacc[e], sca);
+            sb[set].store_e(lds + buf * kBufB + kOpnd, nval, e, sdummy, 1.f);
         }
     };
     // LDS-only barrier: keeps the prefetched global loads in flight
@@ -413,8 +434,8 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
         float sdummy = 0.f;
         auto unit = [&](int u) {
             if (NR_W3_DBG == 3) return;
-            if (u < 4) sa[set].store_e(ia, nval, u, bacc[u]);
-            else sb[set].store_e(ib, nval, u - 4, sdummy);
+            if (u < 4) sa[set].store_e(ia, nval, u, bacc[u], sca);
+            else sb[set].store_e(ib, nval, u - 4, sdummy, 1.f);
         };
         const char* la = lds + buf * kBufB + (m0 + col) * kColB + 16 * h;
         const char* lb = lds + buf * kBufB + kOpnd + (n0 + col) * kColB + 16 * h;
@@ -423,23 +444,29 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
         if (go) {
 #pragma unroll
             for (int j = 0; j < NT; ++j) {
-                bp[j].hi = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB);
-                bp[j].mid = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB + kPlane);
-                bp[j].lo = *reinterpret_cast<const x3::bf16x8*>(lb + 32 * j * kColB + 2 * kPlane);
+                const char* q = lb + 32 * j * kColB;
+                bp[j].hi = *reinterpret_cast<const x3::p8*>(q);
+#if NR_F16
+                bp[j].lo = *reinterpret_cast<const x3::p8*>(q + kPlane);
+#else
+                bp[j].mid = *reinterpret_cast<const x3::p8*>(q + kPlane);
+                bp[j].lo = *reinterpret_cast<const x3::p8*>(q + 2 * kPlane);
+#endif
             }
         }
         constexpr int UPT = (8 + MT - 1) / MT;   // store units per row tile
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             if (go) {
-                const x3::bf16x8 ah = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB);
-                const x3::bf16x8 am = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB + kPlane);
-                const x3::bf16x8 al = *reinterpret_cast<const x3::bf16x8*>(la + 32 * i * kColB + 2 * kPlane);
+                x3::p8 ap[x3::kNP];
+#pragma unroll
+                for (int k = 0; k < x3::kNP; ++k)
+                    ap[k] = *reinterpret_cast<const x3::p8*>(la + 32 * i * kColB + k * kPlane);
 #if NR_W3_MULTI
-                x3::mfma_x6_multi<NT>(ah, am, al, bp, acc[i]);
+                x3::mfma_xp_multi<NT>(ap, bp, acc[i]);
 #else
 #pragma unroll
-                for (int j = 0; j < NT; ++j) acc[i][j] = x3::mfma_x6(ah, am, al, bp[j], acc[i][j]);
+                for (int j = 0; j < NT; ++j) acc[i][j] = x3::mfma_xp(ap, bp[j], acc[i][j]);
 #endif
             }
 #pragma unroll
@@ -450,16 +477,16 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
         // interleave: per row tile, its fragment reads, then each MFMA followed
         // by two VALU ops of the store units, then the units' LDS stores
         if constexpr (WM * WN == 8) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 3 * NT, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, x3::kNP * NT, 0);
 #pragma unroll
             for (int i = 0; i < MT; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, x3::kNP, 0);
 #pragma unroll
-                for (int r = 0; r < 6 * NT; ++r) {
+                for (int r = 0; r < x3::kNProd * NT; ++r) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                     __builtin_amdgcn_sched_group_barrier(0x002, NR_W3_SGB, 0);
                 }
-                __builtin_amdgcn_sched_group_barrier(0x200, 3 * UPT, 0);
+                __builtin_amdgcn_sched_group_barrier(0x200, x3::kNP * UPT, 0);
             }
         }
 #endif
@@ -592,16 +619,19 @@ __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
     const float* p = a.slab + T.slab + e;
     float s = 0.f;
     for (int w = 0; w < T.G; ++w, p += sz) s += *p;
+    if (e < nw) s /= task_scale(a, T);    // exact: a power of two
     grad[dst] = s;
 }
 
 }  // namespace
 
+#if !NR_F16
 NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
     (void)n;
     // upper bound of sum_t G_t * (M_t N_t + M_t) for the task list below
     return (int64_t)(3 * kTargetWG + kTasks) * (256 * 256 + 256) * sizeof(float);
 }
+#endif
 
 namespace {
 int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, float* workspace,
@@ -643,7 +673,7 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     for (int t = 0; t < kTasks; ++t) {
         const int mt = (tasks[t].a.width / tasks[t].wm + 31) / 32;
         const int nt = (tasks[t].b.width / tasks[t].wn + 31) / 32;
-        const int64_t per_tile = x3 ? 384 : 1024;
+        const int64_t per_tile = x3 ? 64 * x3::kNProd : 1024;
         const int64_t mfma = per_tile * mt * nt * (tasks[t].wm * tasks[t].wn > 4 ? 2 : 1);
         const int64_t bytes = (int64_t)(tasks[t].a.width + tasks[t].b.width) * 32 * 4;
         cost[t] = std::max<int64_t>(mfma, bytes / 8) + 512;
@@ -651,7 +681,7 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     }
     // dispatch order: the heavy tasks first; the small ones last and split ~3x
     // finer, so their short workgroups fill the tail of the final round
-    const int64_t heavy = x3 ? 6144 : 16384;
+    const int64_t heavy = x3 ? 1024 * x3::kNProd : 16384;
     int order[kTasks], no = 0;
     for (int pass = 0; pass < 2; ++pass)
         for (int t = 0; t < kTasks; ++t)
@@ -660,6 +690,8 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     int64_t slab = 0;
     // diagnostic: NR_WGRAD_TASKMASK limits the launch to a subset of task ids
     // (the kernel code is unchanged; gradients of the other tasks are then stale)
+    // gradient operand's stats slot (layout.h NR_STATS) of every task id
+    static const int kStat[kTasks] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 8, 9, 9, 10, 10};
     static const long long tmask =
         getenv("NR_WGRAD_TASKMASK") ? strtoll(getenv("NR_WGRAD_TASKMASK"), nullptr, 0) : -1;
     for (int k = 0; k < kTasks; ++k) {
@@ -670,6 +702,7 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
         if (!((tmask >> t) & 1)) g = 0;
         a.task[k] = tasks[t];
         a.task[k].id = t;
+        a.task[k].stat = kStat[t];
         a.task[k].G = (int)g;
         a.task[k].slab = slab;
         slab += g * (tasks[t].a.width * tasks[t].b.width + tasks[t].a.width);
@@ -679,8 +712,13 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     a.n = (int)n;
     a.slab = workspace;
     a.x3 = x3;
+    a.stats = NR_F16 ? SV + nr_sv_stats(nbp) : nullptr;
+#if NR_F16
+    wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+#else
     if (x3) wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else wgrad_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+#endif
     NR_LAUNCH_CHECK("nr_wgrad");
     dim3 rg((256 * 256 + 256 + 255) / 256, kTasks);
     wgrad_reduce_kernel<<<rg, 256, 0, st>>>(a, grad_flat);
@@ -689,12 +727,14 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
 }
 }  // namespace
 
+#if !NR_F16
 NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
                     float* grad_flat, void* stream) {
     return wgrad_launch(false, save, grad_ws, n, workspace, grad_flat, stream);
 }
+#endif
 
-NR_API int nr_wgrad_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+NR_API int NR_X3_NAME(nr_wgrad)(const float* save, const float* grad_ws, int64_t n, float* workspace,
                        float* grad_flat, void* stream) {
     return wgrad_launch(true, save, grad_ws, n, workspace, grad_flat, stream);
 }

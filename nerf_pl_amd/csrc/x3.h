@@ -19,6 +19,19 @@
 // A weight table TAB gives TAB::off(q), the byte offset of group q.
 //
 // wgrad.hip's weight-gradient GEMMs use the 32x32x16 helpers at the end.
+//
+// NR_F16 = 1 builds the same kernels as "f16x3" (the 3xTF32 scheme on CDNA4's
+// fp16 matrix cores): each operand is split into two fp16 pieces x = hi + lo
+// (22 significant bits) and the three products of order <= 2^-11
+// (hi*hi, hi*lo, lo*hi) are accumulated in fp32 on
+// v_mfma_f32_16x16x32_f16 / 32x32x16_f16: half the MFMAs of bf16x6 and 2/3 of
+// its weight bytes.  fp16's 5-bit exponent is handled by exact power-of-two
+// scaling: packed weights carry 2^kWScale (so their lo pieces stay normal),
+// forward activations are split unscaled (|x| < 65504), gradients carry a
+// per-sample scale renormalised layer by layer (mlp_bwd3.hip) and the weight
+// gradient a per-layer scale from the observed maxima (wgrad.hip).  Error per
+// product <= 3 * 2^-22 relative, plus an absolute floor of 2^-25 (fp16
+// subnormal spacing / 2) per operand element.
 #pragma once
 #include <utility>
 #include "layout.h"
@@ -35,19 +48,55 @@
 #ifndef NR_X3_SGB
 #define NR_X3_SGB 1
 #endif
+#ifndef NR_F16
+#define NR_F16 0
+#endif
+// exported C-ABI names of the split-operand entry points: _x3 (bf16x6), _h3 (f16x3)
+#if NR_F16
+#define NR_X3_NAME(base) base##_h3
+#else
+#define NR_X3_NAME(base) base##_x3
+#endif
 
 namespace x3 {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+#if NR_F16
+typedef f16x8 p8;                              // one MFMA operand fragment of a piece
+typedef f16x2 p2;
+typedef _Float16 p1;
+constexpr int kNP = 2;                         // pieces per operand
+constexpr int kNProd = 3;                      // piece products per fp32 product
+constexpr int kWScale = 8;                     // packed weights carry 2^kWScale
+#else
+typedef bf16x8 p8;
+typedef bf16x2 p2;
+typedef __bf16 p1;
+constexpr int kNP = 3;
+constexpr int kNProd = 6;
+constexpr int kWScale = 0;
+#endif
+// 2^-kWScale: takes a layer's accumulator (weights scaled) back to true values
+constexpr float kWUnscale = 1.0f / (float)(1 << kWScale);
+
 constexpr int kWaves = 4;
-constexpr int kTiles = 8;                      // output tiles (16 rows) per k-group
-constexpr int kSlots = 4;                      // ring depth in k-groups
-constexpr int kSlotBytes = 3 * kTiles * 1024;  // 3 pieces x 8 tiles x 1 KiB
+constexpr int kTiles = 8;                          // output tiles (16 rows) per k-group
+// ring depth in k-groups: the DMA of group q is issued kSlots-1 groups before
+// q is consumed, and the wait for it also waits for every older store (vmcnt
+// retires in issue order), so a deeper ring gives the saved-activation stores
+// more time to be acknowledged.  f16x3 groups are 16 KiB: 6 slots fit.
+#ifndef NR_X3_SLOTS
+#define NR_X3_SLOTS (NR_F16 ? 6 : 4)
+#endif
+constexpr int kSlots = NR_X3_SLOTS;
+constexpr int kSlotBytes = kNP * kTiles * 1024;    // pieces x 8 tiles x 1 KiB
 constexpr int kRingBytes = kSlots * kSlotBytes;
-constexpr int kDma = 3 * kTiles / kWaves;      // DMA instructions per wave per group
+constexpr int kDma = kNP * kTiles / kWaves;        // DMA instructions per wave per group
 
 template <int V> using IC = std::integral_constant<int, V>;
 
@@ -103,12 +152,13 @@ __device__ __forceinline__ void stage(const Dma& d) {
     for (int k = 0; k < kDma; ++k) dma_one<TAB, Q, QEND>(d, k);
 }
 
-template <class TAB, int QEND>
+// stages groups 0 .. kSlots-2
+template <class TAB, int QEND, int Q = 0>
 __device__ __forceinline__ void prologue(const Dma& d) {
-    static_assert(kSlots == 4, "prologue stages kSlots-1 groups");
-    stage<TAB, 0, QEND>(d);
-    stage<TAB, 1, QEND>(d);
-    stage<TAB, 2, QEND>(d);
+    if constexpr (Q < kSlots - 1) {
+        stage<TAB, Q, QEND>(d);
+        prologue<TAB, QEND, Q + 1>(d);
+    }
 }
 
 // group Q may be read once this wave's DMA landed and every wave passed here.
@@ -139,23 +189,50 @@ __device__ __forceinline__ void split2(float x0, float x1, bf16x2& hi, bf16x2& m
     const float s0 = r0 - bf16_as_f32(mid, 0), s1 = r1 - bf16_as_f32(mid, 1);
     lo = __builtin_convertvector((f32x2){s0, s1}, bf16x2);
 }
+// f16x3: hi = RN(x) (v_cvt_pk_f16_f32), lo = RN(x - hi); x - hi is exact in fp32
+__device__ __forceinline__ void split2h(float x0, float x1, f16x2& hi, f16x2& lo) {
+    hi = __builtin_convertvector((f32x2){x0, x1}, f16x2);
+    const float r0 = x0 - (float)hi[0], r1 = x1 - (float)hi[1];
+    lo = __builtin_convertvector((f32x2){r0, r1}, f16x2);
+}
 
-struct Pieces { bf16x8 hi, mid, lo; };
+#if NR_F16
+struct Pieces { p8 hi, lo; };
+#else
+struct Pieces { p8 hi, mid, lo; };
+#endif
+
+// pieces of two values as one p2 per piece (k = 0 hi, then mid (bf16x6), lo)
+__device__ __forceinline__ void split_p2(float x0, float x1, p2 (&o)[kNP]) {
+#if NR_F16
+    split2h(x0, x1, o[0], o[1]);
+#else
+    split2(x0, x1, o[0], o[1], o[2]);
+#endif
+}
 
 // elements j = 2p, 2p+1 of a B fragment
 __device__ __forceinline__ void split_pair(float x0, float x1, int p, Pieces& b) {
-    bf16x2 h, m, l;
-    split2(x0, x1, h, m, l);
-    b.hi[2 * p] = h[0]; b.hi[2 * p + 1] = h[1];
-    b.mid[2 * p] = m[0]; b.mid[2 * p + 1] = m[1];
-    b.lo[2 * p] = l[0]; b.lo[2 * p + 1] = l[1];
+    p2 q[kNP];
+    split_p2(x0, x1, q);
+    b.hi[2 * p] = q[0][0]; b.hi[2 * p + 1] = q[0][1];
+#if NR_F16
+    b.lo[2 * p] = q[1][0]; b.lo[2 * p + 1] = q[1][1];
+#else
+    b.mid[2 * p] = q[1][0]; b.mid[2 * p + 1] = q[1][1];
+    b.lo[2 * p] = q[2][0]; b.lo[2 * p + 1] = q[2][1];
+#endif
 }
 
 // pin a value to this point of the instruction stream (the compiler would
 // otherwise sink the next k-step's split down to its first use, after the
 // barrier, where nothing hides it)
 __device__ __forceinline__ void pin(Pieces& p) {
+#if NR_F16
+    asm volatile("" : "+v"(p.hi), "+v"(p.lo));
+#else
     asm volatile("" : "+v"(p.hi), "+v"(p.mid), "+v"(p.lo));
+#endif
 }
 
 // ReLU as an integer max: negative floats (and -0) have the sign bit set
@@ -163,15 +240,14 @@ __device__ __forceinline__ float relu_i(float x) {
     return __int_as_float(max(__float_as_int(x), 0));
 }
 
-// the three weight pieces of one output tile of a k-group
-struct Frag { bf16x8 p[3]; };
+// the weight pieces of one output tile of a k-group
+struct Frag { p8 p[kNP]; };
 
 template <int Q>
 __device__ __forceinline__ void rd_frag(char* ring, int lane, int t, Frag& f) {
     const char* s = slot_ptr(ring, Q) + lane * 16 + t * 1024;
-    f.p[0] = *reinterpret_cast<const bf16x8*>(s);
-    f.p[1] = *reinterpret_cast<const bf16x8*>(s + kTiles * 1024);
-    f.p[2] = *reinterpret_cast<const bf16x8*>(s + 2 * kTiles * 1024);
+#pragma unroll
+    for (int k = 0; k < kNP; ++k) f.p[k] = *reinterpret_cast<const p8*>(s + k * kTiles * 1024);
 }
 
 // hand group Q over (wait + barrier) and read its tile-0 fragments
@@ -183,25 +259,37 @@ __device__ __forceinline__ void enter(char* ring, int lane, Frag& f0) {
     }
 }
 
-__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+__device__ __forceinline__ f32x4 mfma16(const p8& a, const p8& b, f32x4 c) {
+#if NR_F16
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#else
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
 }
 
-// d[S] = c[S] + W * B[S] for both sample tiles: the six products of order
-// <= 2^-16, small terms first, the two accumulators alternating
+// d[S] = c[S] + W * B[S] for both sample tiles: the piece products (bf16x6:
+// six of order <= 2^-16; f16x3: three of order <= 2^-11), small terms first,
+// the two accumulators alternating
 __device__ __forceinline__ void x6_pair(const Frag& w, const Pieces (&b)[2], f32x4 c0, f32x4 c1,
                                         f32x4& d0, f32x4& d1) {
     if constexpr (NR_X3_DBG == 4) {
-        asm volatile("" ::"v"(w.p[0]), "v"(w.p[1]), "v"(w.p[2]), "v"(b[0].hi), "v"(b[1].lo));
+        asm volatile("" ::"v"(w.p[0]), "v"(w.p[kNP - 1]), "v"(b[0].hi), "v"(b[1].lo));
         d0 = c0; d1 = c1;
         return;
     }
+#if NR_F16
+    c0 = mfma16(w.p[1], b[0].hi, c0);  c1 = mfma16(w.p[1], b[1].hi, c1);
+    c0 = mfma16(w.p[0], b[0].lo, c0);  c1 = mfma16(w.p[0], b[1].lo, c1);
+    d0 = mfma16(w.p[0], b[0].hi, c0);  d1 = mfma16(w.p[0], b[1].hi, c1);
+    return;
+#else
     c0 = mfma16(w.p[2], b[0].hi, c0);  c1 = mfma16(w.p[2], b[1].hi, c1);
     c0 = mfma16(w.p[0], b[0].lo, c0);  c1 = mfma16(w.p[0], b[1].lo, c1);
     c0 = mfma16(w.p[1], b[0].mid, c0); c1 = mfma16(w.p[1], b[1].mid, c1);
     c0 = mfma16(w.p[1], b[0].hi, c0);  c1 = mfma16(w.p[1], b[1].hi, c1);
     c0 = mfma16(w.p[0], b[0].mid, c0); c1 = mfma16(w.p[0], b[1].mid, c1);
     d0 = mfma16(w.p[0], b[0].hi, c0);  d1 = mfma16(w.p[0], b[1].hi, c1);
+#endif
 }
 
 // initial accumulator of the first k-step of a layer
@@ -222,7 +310,7 @@ struct BiasInit {     // bias[16F + 4g .. +3] (LDS), the same for both sample ti
 // is done before the last tile's MFMAs, so both the barrier and the first LDS
 // latency of the next group hide under MFMAs in flight.  On exit f0 holds
 // tile 0 of group Q+1.  hook(t) runs inside tile t; its VALU work is
-// interleaved with the tile's 12 MFMAs.
+// interleaved with the tile's 2 kNProd MFMAs.
 template <class TAB, int Q, int QEND, int F0, bool INIT, int EXTRA, typename CInit, typename Hook, int NF>
 __device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][2],
                                          const Pieces (&b)[2], CInit& cinit, Hook& hook, Frag& f0) {
@@ -249,7 +337,7 @@ __device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][
         hook(t);
 #if NR_X3_SGB
 #pragma unroll
-        for (int i = 0; i < 12; ++i) {
+        for (int i = 0; i < 2 * kNProd; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, NR_X3_SGB, 0);  // VALU
         }
@@ -272,8 +360,11 @@ __device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][
 //   Getters declare kStores (a global store per odd unit), sides kBefore7,
 //   the stores they issue in a group before its tile 7 (where the next
 //   group's DMA is waited for).
+// Getters also have begin(producer): called before their first unit once the
+// getter that fed this layer (the producer) has split all of its units.
 struct NoNext {
     static constexpr bool kStores = false;
+    template <typename P> __device__ __forceinline__ void begin(const P&) {}
     template <typename T> __device__ __forceinline__ void operator()(T, int, int, float& x0, float& x1) const {
         x0 = x1 = 0.f;
     }
@@ -337,7 +428,10 @@ __device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)
             const int u = unit_at<NH, HF>(t);
             if (u >= 0) {
                 if constexpr (S + 1 < KS) split_unit(getu, IC<S + 1>(), u, bn);
-                else if constexpr (!IsNoNext<NextU>::value) split_unit(nextu, IC<0>(), u, bn);
+                else if constexpr (!IsNoNext<NextU>::value) {
+                    if (u == 0) nextu.begin(getu);   // getu's splits are complete
+                    split_unit(nextu, IC<0>(), u, bn);
+                }
             }
             side(IC<NH * S + HF>(), t);
         };
@@ -400,33 +494,64 @@ __device__ __forceinline__ float mask_keep(float x, const uint32_t (&w)[4], int 
 }
 
 // ---- 32x32x16 helpers (wgrad.hip) ------------------------------------------
-__device__ __forceinline__ f32x16 mfma_x6(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
-                                          const Pieces& b, f32x16 acc) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b.hi, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b.lo, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b.mid, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b.hi, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b.mid, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b.hi, acc, 0, 0, 0);
+__device__ __forceinline__ f32x16 mfma32(const p8& a, const p8& b, f32x16 c) {
+#if NR_F16
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
+// acc += A * B, small products first; a = the A pieces (hi[, mid], lo)
+__device__ __forceinline__ f32x16 mfma_xp(const p8 (&a)[kNP], const Pieces& b, f32x16 acc) {
+#if NR_F16
+    acc = mfma32(a[1], b.hi, acc);
+    acc = mfma32(a[0], b.lo, acc);
+    acc = mfma32(a[0], b.hi, acc);
+#else
+    acc = mfma32(a[2], b.hi, acc);
+    acc = mfma32(a[0], b.lo, acc);
+    acc = mfma32(a[1], b.mid, acc);
+    acc = mfma32(a[1], b.hi, acc);
+    acc = mfma32(a[0], b.mid, acc);
+    acc = mfma32(a[0], b.hi, acc);
+#endif
     return acc;
 }
 
 // acc[j] += A * B[j] for NJ accumulators sharing the A pieces, product-major
 template <int NJ>
-__device__ __forceinline__ void mfma_x6_multi(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
-                                              const Pieces (&b)[NJ], f32x16* acc) {
+__device__ __forceinline__ void mfma_xp_multi(const p8 (&a)[kNP], const Pieces (&b)[NJ], f32x16* acc) {
+#if NR_F16
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b[j].hi, acc[j], 0, 0, 0);
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[1], b[j].hi, acc[j]);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b[j].lo, acc[j], 0, 0, 0);
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[0], b[j].lo, acc[j]);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b[j].mid, acc[j], 0, 0, 0);
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[0], b[j].hi, acc[j]);
+#else
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, b[j].hi, acc[j], 0, 0, 0);
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[2], b[j].hi, acc[j]);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b[j].mid, acc[j], 0, 0, 0);
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[0], b[j].lo, acc[j]);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b[j].hi, acc[j], 0, 0, 0);
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[1], b[j].mid, acc[j]);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[1], b[j].hi, acc[j]);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[0], b[j].mid, acc[j]);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[0], b[j].hi, acc[j]);
+#endif
+}
+
+// power of two 2^(target - e), e = the binary exponent of m (m in [2^e, 2^(e+1))),
+// shift clamped to [-lim, lim]; 1 for m == 0 (or a non-finite m)
+__device__ __forceinline__ float pow2_norm(float m, int target, int lim) {
+    const int e = (int)((__float_as_uint(m) >> 23) & 0xff) - 127;
+    if (!(m > 0.f) || e == 128) return 1.f;
+    const int sh = min(max(target - e, -lim), lim);
+    return __uint_as_float((uint32_t)(127 + sh) << 23);
 }
 
 }  // namespace x3

@@ -10,6 +10,7 @@ per ``NeRF`` parameter (views into one flat buffer, named_parameters order).
 from __future__ import annotations
 
 import functools
+import os
 
 import torch
 
@@ -23,6 +24,9 @@ def _wgrad_workspace(device_index: int) -> torch.Tensor:
     nbytes = int(lib().nr_wgrad_workspace_bytes(0))
     return torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", device_index))
 
+
+# NERF_PL_AMD_DEBUG=1 keeps the last backward's buffers here (dev/ scripts)
+_DEBUG = {} if os.environ.get("NERF_PL_AMD_DEBUG") == "1" else None
 
 _SHAPES = list(packing.param_shapes().items())
 # parameters the sigma-only graph does not reach (reference autograd leaves them None)
@@ -61,14 +65,14 @@ class _FusedMLP(torch.autograd.Function):
             g_out = g4
         grad_ws = torch.empty(ops.n_blocks(n) * ops.GRAD_PER_BLOCK, device=dev)
         g_out = g_out.contiguous()
-        entry = "nr_mlp_bwd_x3" if packed_b.dtype == torch.uint8 else "nr_mlp_bwd"
-        call(entry, packed_b.data_ptr(), ops.head_ptr(packed_f), out.data_ptr(),
+        call(ops.entry("nr_mlp_bwd", packed_b), packed_b.data_ptr(), ops.head_ptr(packed_f), out.data_ptr(),
              g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), stream_of(dev))
         gflat = torch.empty(packing.N_PARAMS, device=dev)
         ws = _wgrad_workspace(dev.index)
-        call("nr_wgrad_x3" if ops.MATH == "bf16x6" else "nr_wgrad", save.data_ptr(),
-             grad_ws.data_ptr(), n, ws.data_ptr(),
-             gflat.data_ptr(), stream_of(dev))
+        call(ops.entry("nr_wgrad", packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
+             ws.data_ptr(), gflat.data_ptr(), stream_of(dev))
+        if _DEBUG is not None:
+            _DEBUG.update(save=save, grad_ws=grad_ws, g_out=g_out, gflat=gflat, n=n)
         grads, off = [], 0
         for name, shp in _SHAPES:
             k = 1

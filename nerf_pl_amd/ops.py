@@ -16,14 +16,22 @@ from . import packing
 from ._lib import call, lib, ptr, stream_of
 
 BLK = 32                                                # samples per block (one wave)
-# MLP arithmetic: "bf16x6" (fp32 operands split into three bf16 pieces on
-# v_mfma_f32_32x32x16_bf16, fp32-level accuracy, 2.67x the fp32 MFMA rate) or
-# "fp32" (v_mfma_f32_32x32x2_f32).  Both are fp32-accurate; see DESIGN.md.
-MATH = os.environ.get("NERF_PL_AMD_MATH", "bf16x6")
-if MATH not in ("bf16x6", "fp32"):
-    raise ValueError(f"NERF_PL_AMD_MATH must be 'bf16x6' or 'fp32', got {MATH!r}")
-# csrc/layout.h NR_SAVE_PER_BLOCK / NR_GRAD_PER_BLOCK (block-native layout)
+# MLP arithmetic (fp32 operands and results in every case):
+#   "f16x3"  each operand split into two fp16 pieces (hi + lo, 22 bits), the
+#            three products hi*hi + hi*lo + lo*hi accumulated in fp32 on
+#            v_mfma_f32_16x16x32_f16 with power-of-two range scaling (the
+#            3xTF32 scheme on CDNA4); 5.3x the fp32 MFMA issue rate
+#   "bf16x6" three bf16 pieces, six products on v_mfma_f32_16x16x32_bf16
+#            (error <= 2^-25 relative per product); 2.67x
+#   "fp32"   v_mfma_f32_32x32x2_f32
+MATHS = ("f16x3", "bf16x6", "fp32")
+MATH = os.environ.get("NERF_PL_AMD_MATH", "f16x3")
+if MATH not in MATHS:
+    raise ValueError(f"NERF_PL_AMD_MATH must be one of {MATHS}, got {MATH!r}")
+# csrc/layout.h NR_SAVE_PER_BLOCK / NR_GRAD_PER_BLOCK (block-native layout);
+# a save buffer ends with NR_STATS floats (f16x3 gradient statistics)
 SAVE_PER_BLOCK = BLK * (64 + 8 * 256 + 256 + 128 + 32) + 9 * 256
+SAVE_STATS = 16
 GRAD_PER_BLOCK = BLK * (9 * 256 + 128 + 4)
 
 
@@ -65,27 +73,52 @@ def linspace_table(n: int, device_index: int) -> torch.Tensor:
 
 
 @functools.lru_cache(maxsize=None)
-def _maps3(device_index: int):
+def _maps3(device_index: int, np_: int = 3):
     dev = torch.device("cuda", device_index)
-    m, h = packing.build_fwd3_map()
+    m, h = packing.build_fwd3_map(np_)
     return torch.from_numpy(m).to(dev), torch.from_numpy(h).to(dev)
 
 
-FWD3_BYTES = packing.fwd3_offsets()[1]
+FWD3_BYTES = packing.fwd3_offsets(3)[1]
+FWDH3_BYTES = packing.fwd3_offsets(2)[1]
+BWDH3_BYTES = packing.bwd3_bytes(2)
+# C-ABI suffix of the split-operand arithmetics
+_SUFFIX = {"bf16x6": "_x3", "f16x3": "_h3"}
+
+
+def arith_of(packed: torch.Tensor) -> str:
+    """MLP arithmetic a packed (forward or backward) weight buffer was built for."""
+    if packed.dtype != torch.uint8:
+        return "fp32"
+    if packed.numel() in (FWD3_BYTES, packing.BWD3_BYTES):
+        return "bf16x6"
+    if packed.numel() in (FWDH3_BYTES, BWDH3_BYTES):
+        return "f16x3"
+    raise ValueError(f"nerf_pl_amd: unknown packed weight buffer of {packed.numel()} bytes")
+
+
+def entry(base: str, packed: torch.Tensor) -> str:
+    """C-ABI entry point of ``base`` for the arithmetic of ``packed``."""
+    return base + _SUFFIX.get(arith_of(packed), "")
 
 
 def pack_fwd(flat: torch.Tensor, out: torch.Tensor | None = None, math: str | None = None):
-    """Forward weights in the layout of the active MLP arithmetic (``MATH``):
-    float32 fragment order, or the bf16x6 byte buffer (uint8 tensor)."""
-    if (math or MATH) == "bf16x6":
-        return pack_fwd3(flat, out)
+    """Forward weights in the layout of the MLP arithmetic (default ``MATH``):
+    float32 fragment order, or the split-operand byte buffer (uint8 tensor)."""
+    math = math or MATH
+    if math in _SUFFIX:
+        return pack_fwd3(flat, out, math)
     return pack_fwd_fp32(flat, out)
 
 
-def pack_fwd3(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    m, hm = _maps3(flat.device.index)
-    out = torch.empty(FWD3_BYTES, dtype=torch.uint8, device=flat.device) if out is None else out
-    call("nr_pack_x3", ptr(flat), ptr(m), m.numel(), ptr(hm), ptr(out), stream_of(flat.device))
+def pack_fwd3(flat: torch.Tensor, out: torch.Tensor | None = None,
+              math: str = "bf16x6") -> torch.Tensor:
+    np_ = packing.NPIECES[math]
+    m, hm = _maps3(flat.device.index, np_)
+    out = torch.empty(packing.fwd3_offsets(np_)[1], dtype=torch.uint8, device=flat.device) \
+        if out is None else out
+    call("nr_pack" + _SUFFIX[math], ptr(flat), ptr(m), m.numel(), ptr(hm), ptr(out),
+         stream_of(flat.device))
     return out
 
 
@@ -105,17 +138,20 @@ def pack_fwd_fp32(flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.
 
 
 @functools.lru_cache(maxsize=None)
-def _map_bwd3(device_index: int):
-    return torch.from_numpy(packing.build_bwd3_map()).to(torch.device("cuda", device_index))
+def _map_bwd3(device_index: int, np_: int = 3):
+    return torch.from_numpy(packing.build_bwd3_map(np_)).to(torch.device("cuda", device_index))
 
 
 def pack_bwd(flat: torch.Tensor, out: torch.Tensor | None = None, math: str | None = None):
-    """Transposed weights of the data-gradient chain in the active arithmetic."""
-    if (math or MATH) == "bf16x6":
-        m = _map_bwd3(flat.device.index)
-        out = torch.empty(packing.BWD3_BYTES, dtype=torch.uint8, device=flat.device) \
+    """Transposed weights of the data-gradient chain in the arithmetic (default ``MATH``)."""
+    math = math or MATH
+    if math in _SUFFIX:
+        np_ = packing.NPIECES[math]
+        m = _map_bwd3(flat.device.index, np_)
+        out = torch.empty(packing.bwd3_bytes(np_), dtype=torch.uint8, device=flat.device) \
             if out is None else out
-        call("nr_pack_bwd_x3", ptr(flat), ptr(m), m.numel(), ptr(out), stream_of(flat.device))
+        call("nr_pack_bwd" + _SUFFIX[math], ptr(flat), ptr(m), m.numel(), ptr(out),
+             stream_of(flat.device))
         return out
     return pack_bwd_fp32(flat, out)
 
@@ -140,10 +176,9 @@ def mlp_forward(packed: torch.Tensor, *, rays=None, z=None, samples_per_ray=0, x
         n, xstride = z.numel(), 0
     dev = packed.device
     out = torch.empty(n, 1 if sigma_only else 4, device=dev)
-    sv = torch.empty(n_blocks(n) * SAVE_PER_BLOCK, device=dev) if save else None
-    entry = "nr_mlp_fwd_x3" if packed.dtype == torch.uint8 else "nr_mlp_fwd"
-    call(entry, ptr(packed), ptr(rays), ptr(z), n, int(samples_per_ray), ptr(x), xstride,
-         int(sigma_only), ptr(out), ptr(sv), stream_of(dev))
+    sv = torch.empty(n_blocks(n) * SAVE_PER_BLOCK + SAVE_STATS, device=dev) if save else None
+    call(entry("nr_mlp_fwd", packed), ptr(packed), ptr(rays), ptr(z), n, int(samples_per_ray),
+         ptr(x), xstride, int(sigma_only), ptr(out), ptr(sv), stream_of(dev))
     return out, sv
 
 
@@ -151,8 +186,8 @@ def sigma_points(packed, pts):
     """sigma (n,) of the fused sigma-only MLP at points (n,3)."""
     pts = _dev(pts, "pts", 3)
     out = torch.empty(pts.shape[0], device=pts.device)
-    entry = "nr_mlp_sigma_points_x3" if packed.dtype == torch.uint8 else "nr_mlp_sigma_points"
-    call(entry, ptr(packed), ptr(pts), pts.shape[0], ptr(out), stream_of(pts.device))
+    call(entry("nr_mlp_sigma_points", packed), ptr(packed), ptr(pts), pts.shape[0], ptr(out),
+         stream_of(pts.device))
     return out
 
 

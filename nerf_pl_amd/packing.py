@@ -286,24 +286,31 @@ FWD3_LAYERS = OrderedDict([          # name -> (k-steps, output halves)
     ("final", (8, 2)),
     ("dir", (9, 1)),
 ])
+# pieces per operand: 3 for bf16x6 (hi, mid, lo), 2 for f16x3 (hi, lo; the
+# same layout with one piece fewer, csrc/x3.h NR_F16)
+NPIECES = {"bf16x6": 3, "f16x3": 2}
 GROUP_BYTES = 3 * 8 * 1024
 HEAD_BYTES = HEAD_SIZE * 4
 
 
-def fwd3_offsets():
+def group_bytes(np_=3):
+    return np_ * 8 * 1024
+
+
+def fwd3_offsets(np_=3):
     """Byte offset of every layer's first group, and the total buffer size."""
     offs, o = OrderedDict(), HEAD_BYTES
     for k, (ns, nh) in FWD3_LAYERS.items():
         offs[k] = o
-        o += ns * nh * GROUP_BYTES
+        o += ns * nh * group_bytes(np_)
     return offs, o
 
 
-def _group_coords(n):
-    """(piece, tile, lane, j) of every bf16 slot of n groups, and the group."""
-    e = np.arange(n * 3 * 8 * 512)
-    grp = e // (3 * 8 * 512)
-    rem = e % (3 * 8 * 512)
+def _group_coords(n, np_=3):
+    """(piece, tile, lane, j) of every piece slot of n groups, and the group."""
+    e = np.arange(n * np_ * 8 * 512)
+    grp = e // (np_ * 8 * 512)
+    rem = e % (np_ * 8 * 512)
     piece = rem // (8 * 512)
     t = (rem % (8 * 512)) // 512
     lane = (rem % 512) // 8
@@ -311,13 +318,13 @@ def _group_coords(n):
     return grp, piece, t, lane, j
 
 
-def _fwd3_layer_map(w_name, segs, nhalf, offs):
+def _fwd3_layer_map(w_name, segs, nhalf, offs, np_=3):
     """int32 per bf16 slot: flat_index * 4 + piece, or -1 (zero).  segs:
     (k-steps, kind, column offset); groups run k-step major, output half minor."""
     w_off, (rows, fan) = offs[w_name]
     parts = []
     for nks, kind, col0 in segs:
-        grp, piece, t, lane, j = _group_coords(nks * nhalf)
+        grp, piece, t, lane, j = _group_coords(nks * nhalf, np_)
         s, half = grp // nhalf, grp % nhalf
         g = lane >> 4
         row = 128 * half + 16 * t + (lane & 15)
@@ -332,20 +339,21 @@ def _fwd3_layer_map(w_name, segs, nhalf, offs):
     return np.concatenate(parts)
 
 
-def build_fwd3_map():
-    """(group map over every bf16 slot, head map over HEAD_SIZE floats)."""
+def build_fwd3_map(np_=3):
+    """(group map over every piece slot, head map over HEAD_SIZE floats)."""
     offs, _ = param_offsets()
     L = lambda i: f"xyz_encoding_{i}.0.weight"  # noqa: E731
-    parts = [_fwd3_layer_map(L(1), [(2, "pe", 0)], 2, offs)]
+    lm = lambda *a: _fwd3_layer_map(*a, offs, np_)  # noqa: E731
+    parts = [lm(L(1), [(2, "pe", 0)], 2)]
     for i in (2, 3, 4):
-        parts.append(_fwd3_layer_map(L(i), [(8, "acc", 0)], 2, offs))
-    parts.append(_fwd3_layer_map(L(5), [(2, "pe", 0), (8, "acc", XYZ_CH)], 2, offs))
+        parts.append(lm(L(i), [(8, "acc", 0)], 2))
+    parts.append(lm(L(5), [(2, "pe", 0), (8, "acc", XYZ_CH)], 2))
     for i in (6, 7, 8):
-        parts.append(_fwd3_layer_map(L(i), [(8, "acc", 0)], 2, offs))
-    parts.append(_fwd3_layer_map("xyz_encoding_final.weight", [(8, "acc", 0)], 2, offs))
-    parts.append(_fwd3_layer_map("dir_encoding.0.weight", [(8, "acc", 0), (1, "dir", W)], 1, offs))
+        parts.append(lm(L(i), [(8, "acc", 0)], 2))
+    parts.append(lm("xyz_encoding_final.weight", [(8, "acc", 0)], 2))
+    parts.append(lm("dir_encoding.0.weight", [(8, "acc", 0), (1, "dir", W)], 1))
     m = np.concatenate(parts).astype(np.int32)
-    assert m.size * 2 + HEAD_BYTES == fwd3_offsets()[1]
+    assert m.size * 2 + HEAD_BYTES == fwd3_offsets(np_)[1]
     return m, _head_map(offs).astype(np.int32)
 
 
@@ -354,31 +362,35 @@ BWD3_LAYERS = OrderedDict([          # transposed layers: (k-steps over outputs,
     ("L8T", (8, 2)), ("L7T", (8, 2)), ("L6T", (8, 2)), ("L5T", (8, 2)),
     ("L4T", (8, 2)), ("L3T", (8, 2)), ("L2T", (8, 2)),
 ])
-BWD3_BYTES = sum(ns * nh * GROUP_BYTES for ns, nh in BWD3_LAYERS.values())
+def bwd3_bytes(np_=3):
+    return sum(ns * nh * group_bytes(np_) for ns, nh in BWD3_LAYERS.values())
 
 
-def _bwd3_layer_map(w_name, nks, col0, offs):
+BWD3_BYTES = bwd3_bytes(3)
+
+
+def _bwd3_layer_map(w_name, nks, col0, offs, np_=3):
     """Transposed layer: k runs over the forward layer's OUTPUT features
     (kmap16 order), the 16 tiles (two halves of 8) over its input columns
     col0 .. col0+255."""
     w_off, (rows, fan) = offs[w_name]
-    grp, piece, t, lane, j = _group_coords(nks * 2)
+    grp, piece, t, lane, j = _group_coords(nks * 2, np_)
     s, half = grp // 2, grp % 2
     k_out = kmap16(s, lane >> 4, j)
     c_in = col0 + 128 * half + 16 * t + (lane & 15)
     return (w_off + k_out * fan + c_in) * 4 + piece
 
 
-def build_bwd3_map():
+def build_bwd3_map(np_=3):
     offs, _ = param_offsets()
     L = lambda i: f"xyz_encoding_{i}.0.weight"  # noqa: E731
-    parts = [_bwd3_layer_map("dir_encoding.0.weight", 4, 0, offs),
-             _bwd3_layer_map("xyz_encoding_final.weight", 8, 0, offs)]
+    lm = lambda *a: _bwd3_layer_map(*a, offs, np_)  # noqa: E731
+    parts = [lm("dir_encoding.0.weight", 4, 0), lm("xyz_encoding_final.weight", 8, 0)]
     for i in (8, 7, 6):
-        parts.append(_bwd3_layer_map(L(i), 8, 0, offs))
-    parts.append(_bwd3_layer_map(L(5), 8, XYZ_CH, offs))
+        parts.append(lm(L(i), 8, 0))
+    parts.append(lm(L(5), 8, XYZ_CH))
     for i in (4, 3, 2):
-        parts.append(_bwd3_layer_map(L(i), 8, 0, offs))
+        parts.append(lm(L(i), 8, 0))
     m = np.concatenate(parts).astype(np.int32)
-    assert m.size * 2 == BWD3_BYTES
+    assert m.size * 2 == bwd3_bytes(np_)
     return m

@@ -15,8 +15,8 @@ step() {  # step <name> <timeout-seconds> <cmd...>
 n=0
 for s in "$@"; do
     case $s in
-        tests) step tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
-        testsall) step testsall 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+        tests) step tests 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+        testsall) step testsall 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
         benchq) step benchq 300 python bench.py --steps 10 --warmup 3 --cpu-baseline-seconds 0 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-baseline-seconds 0 --no-kernel-timing ;;

@@ -88,7 +88,34 @@ def test_pack_x3_pieces():
     assert np.all(np.abs(recon - fl) <= 2.0 ** -24 * np.abs(fl))
 
 
-MATHS = ["fp32", "bf16x6"]
+def test_pack_h3_pieces():
+    """f16x3 buffer: fp32 head block (layer biases x 2^8), then for every
+    weight w' = 256 w its two fp16 pieces hi = f16(w'), lo = f16(w' - hi)."""
+    from nerf_pl_amd import ops, packing
+    p = O.make_params(6)
+    flat = flat_params(p)
+    buf = ops.pack_fwd3(flat, math="f16x3").cpu()
+    m, hm = packing.build_fwd3_map(2)
+    head = buf[:packing.HEAD_BYTES].view(torch.float32).numpy()
+    fl = flat.cpu().numpy()
+    sc = np.where(np.arange(hm.size) < 8 * 256 + 256 + 128, 256.0, 1.0).astype(np.float32)
+    np.testing.assert_array_equal(head, np.where(hm >= 0, fl[np.maximum(hm, 0)] * sc, 0))
+    pieces = buf[packing.HEAD_BYTES:].view(torch.float16).float().numpy()
+    assert pieces.size == m.size
+    w = torch.from_numpy(fl) * 256
+    hi = w.to(torch.float16).float()
+    lo = (w - hi).to(torch.float16).float()
+    ref = torch.stack([hi, lo], 1).numpy()
+    ok = m >= 0
+    np.testing.assert_array_equal(pieces[ok], ref[m[ok] >> 2, m[ok] & 3])
+    assert np.all(pieces[~ok] == 0)
+    recon = ref.astype(np.float64).sum(1) / 256
+    big = np.abs(fl) > 2.0 ** -10      # below, the lo piece is an fp16 subnormal
+    assert np.all(np.abs(recon - fl)[big] <= 2.0 ** -22 * np.abs(fl)[big])
+    assert np.all(np.abs(recon - fl) <= 2.0 ** -22 * np.abs(fl) + 2.0 ** -33)
+
+
+MATHS = ["fp32", "bf16x6", "f16x3"]
 
 
 @pytest.mark.parametrize("math", MATHS)
@@ -157,7 +184,7 @@ def test_mlp_forward_saved_activations(math):
                                                  p["dir_encoding.0.weight"],
                                                  p["dir_encoding.0.bias"]))
     seg = ops.save_segments(sv, n)
-    if math == "bf16x6":
+    if math in ("bf16x6", "f16x3"):
         _check_saved_n16(seg, n, e_xyz, e_dir, hs, feat, hdir)
         return
     pe = ops.pe_to_rows(seg["pe"], n, 32)
