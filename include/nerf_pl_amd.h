@@ -53,8 +53,9 @@ int nr_embed(const float* x, int64_t n, int n_freqs, float* out, void* stream);
  *   Embedded path (x != NULL): x is (n, xstride) pre-embedded [xyz_emb(63),
  *     dir_emb(27)] or xyz_emb only when sigma_only (NeRF.forward(x) API).
  *   out: (n,4) [rgb, sigma] or (n,1) sigma when sigma_only.
- *   save: NULL for inference, else nr_blocks_pad(n)*nr_layout_query(3) + 16
- *     floats of activations kept for nr_mlp_bwd / nr_wgrad (training). */
+ *   save: NULL for inference, else nr_blocks_pad(n) * (nr_layout_query(3) + 11) + 16
+ *     floats: activations kept for nr_mlp_bwd / nr_wgrad (training), then the
+ *     f16x3 gradient statistics (layout.h nr_stats_floats). */
 int nr_mlp_fwd(const float* packed_fwd, const float* rays, const float* z, int64_t n,
                int samples_per_ray, const float* x, int xstride, int sigma_only, float* out,
                float* save, void* stream);
@@ -91,9 +92,9 @@ int nr_mlp_bwd_x3(const void* packed_bwd, const float* head, const float* out, c
  * of their *_x3 twins; buffers: forward nr_fwd3_packed_bytes_h3() = 2,388,000
  * bytes (fp32 head block with the layer biases x 2^8, then fp16 k-groups of
  * packing.build_fwd3_map(2)), backward 2,228,224 bytes (build_bwd3_map(2)).
- * A training save buffer (nr_mlp_fwd_h3 with save) carries 16 floats after
- * the activations (layout.h NR_STATS) that the forward zeroes, nr_mlp_bwd_h3
- * fills with gradient maxima and nr_wgrad_h3 reads. */
+ * A training save buffer carries, after the activations, the gradient
+ * statistics (layout.h nr_stats_floats): nr_mlp_bwd_h3 writes per-wave maxima,
+ * nr_wgrad_h3 reduces and uses them. */
 int64_t nr_fwd3_packed_bytes_h3(void);
 int nr_pack_h3(const float* flat, const int32_t* map, int64_t n, const int32_t* head_map,
                void* out, void* stream);

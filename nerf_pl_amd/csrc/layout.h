@@ -102,11 +102,17 @@ __host__ __device__ __forceinline__ int64_t nr_sv_dirpe(int64_t nb) {
 __host__ __device__ __forceinline__ int64_t nr_sv_mask(int64_t nb) {
     return nr_sv_dirpe(nb) + NR_NATIVE(32) * nb;
 }
-// f16x3 statistics after the saved activations of a training forward (16
-// floats, zeroed by the forward): [l] = max |true gradient| of gradient segment
-// l (0..7 dz1..dz8, 8 dfeat, 9 dzdir, 10 dhead), as uint bits for atomicMax
+// f16x3 statistics after the saved activations of a training forward:
+// NR_STATS floats [l] = max |true gradient| of gradient segment l (0..7
+// dz1..dz8, 8 dfeat, 9 dzdir, 10 dhead), then the per-wave maxima
+// [l][nb] they reduce (mlp_bwd3.hip writes those with plain stores -- no
+// contended atomics -- and wgrad.hip reduces them)
 #define NR_STATS 16
+#define NR_STAT_SEGS 11
 __host__ __device__ __forceinline__ int64_t nr_sv_stats(int64_t nb) { return NR_SAVE_PER_BLOCK * nb; }
+__host__ __device__ __forceinline__ int64_t nr_stats_floats(int64_t nb) {
+    return NR_STATS + NR_STAT_SEGS * nb;
+}
 __host__ __device__ __forceinline__ int64_t nr_gd_dz(int l, int64_t nb) {   // l = 0..8 (8 = dfeat)
     return (int64_t)l * NR_NATIVE(256) * nb;
 }

@@ -38,7 +38,7 @@ static_assert(BwdTab::off(kQ) == (NR_F16 ? 2228224 : 3342336),
 // renormalisation as a bound (GradU::inj).  Stored gradients are true values.
 constexpr int kGT = 6;
 constexpr int kGLim = 64;      // largest renormalisation step (binades)
-constexpr int kSigLim = 96;    // |log2 sigma| bound
+constexpr int kSigLim = 120;   // |log2 sigma| bound
 struct GScale {
     float ks[2] = {1.f, 1.f};    // accumulator -> B value
     float kst[2] = {1.f, 1.f};   // accumulator -> true value (stored)
@@ -70,11 +70,12 @@ __device__ __forceinline__ void gscale_from(GScale& sc, const GScale& prod, cons
     }
 }
 
-// max |true gradient| of a segment over the wave -> stats (atomicMax on the bits)
-__device__ __forceinline__ void report_max(float m, float* stats, int lane) {
+// max |true gradient| of a segment over the wave -> its per-wave slot
+// (layout.h NR_STAT_SEGS; reduced by wgrad.hip)
+__device__ __forceinline__ void report_max(float m, float* slot, int lane) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if (lane == 0) atomicMax(reinterpret_cast<unsigned*>(stats), __float_as_uint(m));
+    if (lane == 0) *slot = m;
 }
 
 // B units of a gradient input dz (NF feature tiles): with MASK the ReLU mask
@@ -122,10 +123,10 @@ struct GradU {
             store_n16(f32x4{pend[0], pend[1], t0, t1}, F, sb, dst, lane);
         }
     }
-    // after the last split: the segment's max |true value| -> stats
-    __device__ __forceinline__ void report(float* stats) const {
+    // after the last split: the segment's max |true value| -> its stats slot
+    __device__ __forceinline__ void report(float* slot) const {
         if constexpr (NR_F16)
-            report_max(fmaxf(sc.mx[0] / sc.sig[0], sc.mx[1] / sc.sig[1]), stats, lane);
+            report_max(fmaxf(sc.mx[0] / sc.sig[0], sc.mx[1] / sc.sig[1]), slot, lane);
     }
 };
 
@@ -145,7 +146,7 @@ struct Bwd3Args {
     const float* out; const float* g_out; const float* save;
     int n;
     float* grad;
-    float* stats;    // f16x3: layout.h nr_sv_stats (inside the save buffer)
+    float* stats;    // f16x3: per-wave maxima [NR_STAT_SEGS][nb] (layout.h, in the save buffer)
 };
 
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
@@ -220,7 +221,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         for (int S = 0; S < 2; ++S)
             m = fmaxf(m, fmaxf(fmaxf(fabsf(dzr[S][0]), fabsf(dzr[S][1])),
                                fmaxf(fabsf(dzr[S][2]), fabsf(dsig[S]))));
-        report_max(m, a.stats + 10, lane);
+        report_max(m, a.stats + 10 * nb + blk, lane);
     }
 
     // d hdir = W_rgb^T dz_rgb, masked by the dir-layer ReLU -> dz_dir (128)
@@ -254,7 +255,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         const uint4 m = mask[l * 64];
         w[0] = m.x; w[1] = m.y; w[2] = m.z; w[3] = m.w;
     };
-    float* const ST = a.stats;
+    float* const STW = a.stats + blk;     // + l * nb: this wave's slot of segment l
 #define NR_GRADU(NAME, X, DZ, ML)                                   \
     GradU<16, true> NAME{X, dzseg(DZ), {0u, 0u, 0u, 0u}, lane};     \
     mwords(ML, NAME.mw);
@@ -293,7 +294,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     }
     split_all(uc, b);
     segment<BwdTab, kDirT, 4, 2, kQ, true>(dma, lane, A, uc, ua, zero, none, b, f0);
-    uc.report(ST + 9);
+    uc.report(STW + 9 * nb);
     // d h8 = W_final^T dfeat + W_sigma^T dsigma; dz8 = d h8 * [h8 > 0]
     NR_GRADU(u8, B, 7, 7)
     if constexpr (NR_F16) {
@@ -302,31 +303,33 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     }
     {
         // the accumulator carries 2^kWScale sigma(dfeat) (f16x3), so does its C operand
-        const float c0 = (float)(1 << kWScale) * ua.sc.sig[0], c1 = (float)(1 << kWScale) * ua.sc.sig[1];
-        SigInit si{H + NR_H_WSIG, g, NR_F16 ? dsig[0] * c0 : dsig[0], NR_F16 ? dsig[1] * c1 : dsig[1]};
+        // (dsigma * sigma first: 2^kWScale * sigma alone may overflow when dsigma is 0)
+        constexpr float kW = (float)(1 << kWScale);
+        SigInit si{H + NR_H_WSIG, g, NR_F16 ? dsig[0] * ua.sc.sig[0] * kW : dsig[0],
+                   NR_F16 ? dsig[1] * ua.sc.sig[1] * kW : dsig[1]};
         segment<BwdTab, kFinalT, 8, 2, kQ, true>(dma, lane, B, ua, u8, si, none, b, f0);
     }
-    ua.report(ST + 8);
+    ua.report(STW + 8 * nb);
     NR_GRADU(u7, A, 6, 6)
     segment<BwdTab, kL8T, 8, 2, kQ, true>(dma, lane, A, u8, u7, zero, none, b, f0);
-    u8.report(ST + 7);
+    u8.report(STW + 7 * nb);
     NR_GRADU(u6, B, 5, 5)
     segment<BwdTab, kL7T, 8, 2, kQ, true>(dma, lane, B, u7, u6, zero, none, b, f0);
-    u7.report(ST + 6);
+    u7.report(STW + 6 * nb);
     NR_GRADU(u5, A, 4, 4)
     segment<BwdTab, kL6T, 8, 2, kQ, true>(dma, lane, A, u6, u5, zero, none, b, f0);
-    u6.report(ST + 5);
+    u6.report(STW + 5 * nb);
     NR_GRADU(u4, B, 3, 3)   // through the h4 columns of the skip layer
     segment<BwdTab, kL5T, 8, 2, kQ, true>(dma, lane, B, u5, u4, zero, none, b, f0);
-    u5.report(ST + 4);
+    u5.report(STW + 4 * nb);
     NR_GRADU(u3, A, 2, 2)
     segment<BwdTab, kL4T, 8, 2, kQ, true>(dma, lane, A, u4, u3, zero, none, b, f0);
-    u4.report(ST + 3);
+    u4.report(STW + 3 * nb);
     NR_GRADU(u2, B, 1, 1)
     segment<BwdTab, kL3T, 8, 2, kQ, true>(dma, lane, B, u3, u2, zero, none, b, f0);
-    u3.report(ST + 2);
+    u3.report(STW + 2 * nb);
     segment<BwdTab, kL2T, 8, 2, kQ, true>(dma, lane, A, u2, nonext, zero, none, b, f0);
-    u2.report(ST + 1);
+    u2.report(STW + 1 * nb);
 #undef NR_GRADU
     {   // dz1 = (W2^T dz2) * [h1 > 0]
         uint32_t mw[4];
@@ -349,7 +352,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
                 }
                 store_n16(v, F, S, d1, lane);
             }
-        if constexpr (NR_F16) report_max(m1, ST + 0, lane);
+        if constexpr (NR_F16) report_max(m1, STW, lane);
     }
 }
 
@@ -399,7 +402,7 @@ NR_API int NR_X3_NAME(nr_mlp_bwd)(const void* packed_bwd, const float* head, con
     NR_REQUIRE((((uintptr_t)save | (uintptr_t)grad_ws | (uintptr_t)g_out | (uintptr_t)out |
                  (uintptr_t)packed_bwd | (uintptr_t)head) & 15) == 0,
                "nr_mlp_bwd_x3: buffers must be 16-byte aligned");
-    float* stats = const_cast<float*>(save) + nr_sv_stats(nr_blocks_pad(n));
+    float* stats = const_cast<float*>(save) + nr_sv_stats(nr_blocks_pad(n)) + NR_STATS;
     Bwd3Args a{reinterpret_cast<const char*>(packed_bwd), head, out, g_out, save, (int)n, grad_ws,
                stats};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));

@@ -323,10 +323,6 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         }
     }
 
-    if constexpr (SAVE && NR_F16) {   // gradient statistics of the backward (layout.h)
-        if (blockIdx.x == 0 && threadIdx.x < NR_STATS) SV[nr_sv_stats(nb) + threadIdx.x] = 0.f;
-    }
-
     Frag f0;           // tile-0 fragments of the next k-group
     enter<0, QEND>(smem, lane, f0);
 

@@ -90,7 +90,7 @@ struct WgArgs {
 __device__ __forceinline__ float task_scale(const WgArgs& a, const WgTask& T) {
 #if NR_F16
     constexpr int kWT = 14;
-    return x3::pow2_norm(a.stats[T.stat], kWT, 100);
+    return x3::pow2_norm(a.stats[T.stat], kWT, 126);
 #else
     (void)a; (void)T;
     return 1.f;
@@ -607,6 +607,24 @@ __device__ int wgrad_bias_dest(int t, int o) {
     return -1;
 }
 
+#if NR_F16
+// stats[l] = max over the per-wave maxima [l][nb] written by mlp_bwd3.hip
+__global__ void stats_reduce_kernel(float* __restrict__ stats, int nb) {
+    const int l = blockIdx.x;
+    const float* w = stats + NR_STATS + (int64_t)l * nb;
+    float m = 0.f;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) m = fmaxf(m, w[i]);
+    __shared__ float red[256];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) stats[l] = red[0];
+}
+#endif
+
 __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
     const int t = blockIdx.y;
     const WgTask& T = a.task[t];
@@ -714,6 +732,8 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     a.x3 = x3;
     a.stats = NR_F16 ? SV + nr_sv_stats(nbp) : nullptr;
 #if NR_F16
+    stats_reduce_kernel<<<NR_STAT_SEGS, 256, 0, st>>>(SV + nr_sv_stats(nbp), (int)nbp);
+    NR_LAUNCH_CHECK("nr_wgrad_stats");
     wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #else
     if (x3) wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);

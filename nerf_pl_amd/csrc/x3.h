@@ -39,7 +39,8 @@
 // NR_X3_DBG (timing experiments only, never in the shipped build):
 // 1 = no barrier, 2 = no DMA wait and no barrier, 3 = no DMA at all,
 // 4 = no MFMA (fragments still read), 5 = no B split between k-steps,
-// 8 = clock stamps (mlp_fwd3.hip writes s_memtime / s_memrealtime deltas)
+// 8 = clock stamps (mlp_fwd3.hip writes s_memtime / s_memrealtime deltas),
+// 9 = no saved-activation / gradient stores (store_n16)
 #ifndef NR_X3_DBG
 #define NR_X3_DBG 0
 #endif
@@ -477,9 +478,23 @@ __device__ __forceinline__ float acc_b(const f32x4 (&X)[NF][2], int s, int sb, i
 // Width-W segment of a 32-sample block: [F = W/16][S 2][lane 64][4] floats,
 // element (F, S, l, r) = feature 16F + 4(l >> 4) + r of sample 16S + (l & 15):
 // one wave store of acc[F][S] moves a contiguous 1 KiB.
+// saved activations / gradients are written with non-temporal stores: they
+// are re-read only by a later kernel, and streaming them past L2 keeps the
+// weight ring's L2 lines resident (f16x3 fine pass: fwd+save 2.86 -> 2.63 ms,
+// dgrad 3.07 -> 2.56 ms)
+#ifndef NR_NT_STORE
+#define NR_NT_STORE 1
+#endif
 __device__ __forceinline__ void store_n16(const f32x4& v, int F, int S, float* __restrict__ blk,
                                           int lane) {
-    *reinterpret_cast<f32x4*>(blk + ((F * 2 + S) * 64 + lane) * 4) = v;
+    f32x4* p = reinterpret_cast<f32x4*>(blk + ((F * 2 + S) * 64 + lane) * 4);
+#if NR_X3_DBG == 9
+    asm volatile("" ::"v"(v), "v"(p));     // timing experiment: no stores
+#elif NR_NT_STORE
+    __builtin_nontemporal_store(v, p);     // streamed: keep L2 for the weight ring
+#else
+    *p = v;
+#endif
 }
 
 // ReLU mask bits of a post-ReLU activation: word F >> 2 of the lane, bit

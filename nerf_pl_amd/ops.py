@@ -29,9 +29,16 @@ MATH = os.environ.get("NERF_PL_AMD_MATH", "f16x3")
 if MATH not in MATHS:
     raise ValueError(f"NERF_PL_AMD_MATH must be one of {MATHS}, got {MATH!r}")
 # csrc/layout.h NR_SAVE_PER_BLOCK / NR_GRAD_PER_BLOCK (block-native layout);
-# a save buffer ends with NR_STATS floats (f16x3 gradient statistics)
+# a save buffer ends with the f16x3 gradient statistics (nr_stats_floats:
+# NR_STATS reduced maxima, then NR_STAT_SEGS per-wave maxima per block)
 SAVE_PER_BLOCK = BLK * (64 + 8 * 256 + 256 + 128 + 32) + 9 * 256
-SAVE_STATS = 16
+SAVE_STATS, STAT_SEGS = 16, 11
+
+
+def save_floats(n: int) -> int:
+    """Floats of a training save buffer for n samples."""
+    nb = n_blocks(n)
+    return nb * SAVE_PER_BLOCK + SAVE_STATS + STAT_SEGS * nb
 GRAD_PER_BLOCK = BLK * (9 * 256 + 128 + 4)
 
 
@@ -176,7 +183,7 @@ def mlp_forward(packed: torch.Tensor, *, rays=None, z=None, samples_per_ray=0, x
         n, xstride = z.numel(), 0
     dev = packed.device
     out = torch.empty(n, 1 if sigma_only else 4, device=dev)
-    sv = torch.empty(n_blocks(n) * SAVE_PER_BLOCK + SAVE_STATS, device=dev) if save else None
+    sv = torch.empty(save_floats(n), device=dev) if save else None
     call(entry("nr_mlp_fwd", packed), ptr(packed), ptr(rays), ptr(z), n, int(samples_per_ray),
          ptr(x), xstride, int(sigma_only), ptr(out), ptr(sv), stream_of(dev))
     return out, sv

@@ -1,6 +1,7 @@
 """Isolated timing of the fused MLP kernels at the cfg2 fine-pass size
 (786,432 samples), for profiling (dev tool).
-Usage: kbench.py [fwd|fwdsave|fwd3|fwd3save|bwd|wgrad|all] [reps]"""
+Usage: kbench.py [fwd|fwdsave|fwd3|fwd3save|bwd|bwd3|wgrad|wgrad3|fwdh3|fwdh3save|bwdh3|wgradh3
+                  |all|h3] [reps]   (x3 = bf16x6, h3 = f16x3)"""
 import os
 import sys
 import time
@@ -13,8 +14,10 @@ from nerf_pl_amd._lib import call, stream_of
 from nerf_pl_amd.functions import _wgrad_workspace
 
 FLOP = {"fwd": 1186816, "fwdsave": 1186816, "fwd3": 1186816, "fwd3save": 1186816,
-        "bwd": 1115392, "bwd3": 1115392, "wgrad": 1186816, "wgrad3": 1186816}
+        "bwd": 1115392, "bwd3": 1115392, "wgrad": 1186816, "wgrad3": 1186816,
+        "fwdh3": 1186816, "fwdh3save": 1186816, "bwdh3": 1115392, "wgradh3": 1186816}
 PEAK3 = 2516.6 / 6     # bf16 dense MFMA peak / 6 products: fp32-equivalent ceiling of bf16x6
+PEAKH3 = 2516.6 / 3    # fp16 dense MFMA peak / 3 products: ceiling of f16x3
 
 
 def main():
@@ -25,6 +28,7 @@ def main():
     flat = (torch.rand(packing.N_PARAMS, device=dev) - 0.5) * 0.15
     pf, pb = ops.pack_fwd_fp32(flat), ops.pack_bwd_fp32(flat)
     p3, pb3 = ops.pack_fwd3(flat), ops.pack_bwd(flat, math="bf16x6")
+    ph3, pbh3 = ops.pack_fwd3(flat, math="f16x3"), ops.pack_bwd(flat, math="f16x3")
     n_rays, spr = 4096, 192
     n = n_rays * spr
     rays = torch.randn(n_rays, 8, device=dev)
@@ -59,12 +63,28 @@ def main():
                  sv.data_ptr(), n, gw.data_ptr(), st)
         elif k == "wgrad3":
             call("nr_wgrad_x3", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
+        elif k in ("fwdh3", "fwdh3save"):
+            call("nr_mlp_fwd_h3", ph3.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0,
+                 0, out.data_ptr(), sv.data_ptr() if k == "fwdh3save" else None, st)
+        elif k == "bwdh3":
+            call("nr_mlp_bwd_h3", pbh3.data_ptr(), ops.head_ptr(ph3), out.data_ptr(),
+                 gout.data_ptr(), sv.data_ptr(), n, gw.data_ptr(), st)
+        elif k == "wgradh3":
+            call("nr_wgrad_h3", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
         elif k == "wgrad":
             call("nr_wgrad", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
 
-    ks = ["fwd", "fwdsave", "fwd3", "fwd3save", "bwd", "bwd3", "wgrad", "wgrad3"] if which == "all" \
-        else which.split(",")
-    run("bwd")
+    if which == "all":
+        ks = ["fwd", "fwdsave", "fwd3", "fwd3save", "bwd", "bwd3", "wgrad", "wgrad3"]
+    elif which == "h3":
+        ks = ["fwdh3", "fwdh3save", "bwdh3", "wgradh3"]
+    else:
+        ks = which.split(",")
+    if any("h3" in k for k in ks):   # f16x3: save buffer (and its statistics) by the h3 forward
+        run("fwdh3save")
+        run("bwdh3")
+    else:
+        run("bwd")
     for k in ks:
         for _ in range(2):
             run(k)
@@ -77,7 +97,8 @@ def main():
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         tf = n * FLOP[k] / (ms * 1e-3) / 1e12
-        extra = f"  {tf / PEAK3 * 100:5.1f}% of the bf16x6 ceiling" if "3" in k else ""
+        extra = (f"  {tf / PEAKH3 * 100:5.1f}% of the f16x3 ceiling" if "h3" in k else
+                 f"  {tf / PEAK3 * 100:5.1f}% of the bf16x6 ceiling" if "3" in k else "")
         print(f"{k:8s} {ms:8.3f} ms  {tf:6.1f} TFLOP/s  {tf / 157.3 * 100:5.1f}% of fp32 MFMA peak"
               + extra, flush=True)
 

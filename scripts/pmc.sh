@@ -12,7 +12,7 @@ for ctrs in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
             "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
             "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE TA_BUSY_avr"; do
     i=$((i+1))
-    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctrs -d $out/p$i -o run --output-format csv -- python scripts/kbench.py $k 3 > $out/p$i.log 2>&1
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctrs -d $out/p$i -o run --output-format csv -- python scripts/kbench.py $k ${REPS:-3} > $out/p$i.log 2>&1
     rc=$?
     echo "pass $i ($ctrs) rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 $out/p$i.log; fi
