@@ -43,6 +43,46 @@ FLOP_FWD = 1_186_816
 FLOP_DGRAD = 1_115_392
 FLOP_WGRAD = 1_186_816
 FLOP_TRAIN = FLOP_FWD + FLOP_DGRAD + FLOP_WGRAD   # 3,489,024
+# weight gradient: algorithmic HBM bytes per sample (every saved segment read once)
+BYTES_WGRAD = 4 * (2528 + 2436)                     # 19,856
+
+
+def kernel_roofline(k, events, math, traffic_json):
+    """Roofline of one MLP kernel from its largest (fine-pass) launches, timed
+    with HIP events on the stream it runs on.  The weight gradient streams every
+    saved segment once at 60 FLOP/B: HBM-bound (algorithmic bytes); the fused forward and data-gradient chains are MFMA-
+    bound (algorithmic FLOPs of the fp32 products)."""
+    big = [(s.elapsed_time(e), n) for s, e, n in events]
+    nmax = max(n for _, n in big)
+    durs = [t for t, n in big if n == nmax]
+    avg = sum(durs) / len(durs)
+    flops = {"mlp_fwd": FLOP_FWD, "mlp_bwd_dgrad": FLOP_DGRAD, "mlp_wgrad": FLOP_WGRAD}[k]
+    tflops = flops * nmax / (avg * 1e-3) / 1e12
+    traffic, tsrc = None, None
+    t = traffic_json.get(f"{math}/{k}") or traffic_json.get(k)
+    if t and int(t["samples"]) == nmax and t.get("arithmetic", math) == math:
+        traffic = round(t["hbm_bytes"] / 1e9, 3)
+        tsrc = f"profiles/r01/traffic.json ({t['method']})"
+    common = dict(kernel=k, traffic=traffic, traffic_unit="GB per launch", traffic_source=tsrc,
+                  samples_per_launch=nmax, avg_launch_ms=round(avg, 4))
+    if k == "mlp_wgrad":
+        ach = BYTES_WGRAD * nmax / (avg * 1e-3) / 1e9
+        return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(ach / HBM_PEAK_GBS, 4), bytes_per_sample=BYTES_WGRAD,
+                    bytes_basis="every saved activation (2528 floats/sample) and gradient "
+                                "(2436 floats/sample) segment read once",
+                    tflops_fp32_equiv=round(tflops, 2), **common)
+    np_ = SPLIT_PRODUCTS.get(math)
+    peak = BF16_MFMA_PEAK_TF / np_ if np_ else FP32_MFMA_PEAK_TF
+    basis = {
+        "bf16x6": "bf16x6: fp32 FLOPs on v_mfma_f32_16x16x32_bf16, six bf16 products per "
+                  f"fp32 product -> ceiling = dense bf16 peak {BF16_MFMA_PEAK_TF:.0f} / 6",
+        "f16x3": "f16x3: fp32 FLOPs on v_mfma_f32_16x16x32_f16, three fp16 products per "
+                 f"fp32 product -> ceiling = dense fp16 peak {BF16_MFMA_PEAK_TF:.0f} / 3",
+    }.get(math, "fp32: v_mfma_f32_32x32x2_f32 dense peak")
+    return dict(bound="mfma", achieved=round(tflops, 2), peak=round(peak, 1), unit="TFLOP/s",
+                frac=round(tflops / peak, 4), flop_per_sample=flops, peak_basis=basis,
+                frac_of_fp32_mfma_peak=round(tflops / FP32_MFMA_PEAK_TF, 4), **common)
 
 
 def _math():
@@ -222,42 +262,19 @@ def main():
     rays_per_s = args.batch * world * args.steps / el
 
     ks = timer.summary()
-    roof = None
+    roof, roofs = None, {}
     if ks:
-        flop = {"mlp_fwd": FLOP_FWD, "mlp_bwd_dgrad": FLOP_DGRAD, "mlp_wgrad": FLOP_WGRAD}
-        dom = max((k for k in ks if k in flop), key=lambda k: ks[k]["total_ms"])
-        d = ks[dom]
-        # the dominant kernel's largest launches (fine pass) set the roofline
-        big = [(s.elapsed_time(e), n) for s, e, n in timer.events[dom]]
-        nmax = max(n for _, n in big)
-        durs = [t for t, n in big if n == nmax]
-        avg = sum(durs) / len(durs)
-        ach = flop[dom] * nmax / (avg * 1e-3) / 1e12
-        traffic, tsrc = None, None
         math = _math()
-        # PMC-measured HBM bytes of this kernel and arithmetic (scripts/traffic.py)
+        tj = {}
         tf = os.path.join(REPO, "profiles", "r01", "traffic.json")
         if os.path.exists(tf):
             tj = json.load(open(tf))
-            t = tj.get(f"{math}/{dom}") or tj.get(dom)
-            if t and int(t["samples"]) == nmax and t.get("arithmetic", math) == math:
-                traffic = round(t["hbm_bytes"] / 1e9, 3)
-                tsrc = f"profiles/r01/traffic.json ({t['method']})"
-        np_ = SPLIT_PRODUCTS.get(math)
-        peak = BF16_MFMA_PEAK_TF / np_ if np_ else FP32_MFMA_PEAK_TF
-        basis = {
-            "bf16x6": "bf16x6: fp32 FLOPs on v_mfma_f32_16x16x32_bf16, six bf16 products per "
-                      f"fp32 product -> ceiling = dense bf16 peak {BF16_MFMA_PEAK_TF:.0f} / 6",
-            "f16x3": "f16x3: fp32 FLOPs on v_mfma_f32_16x16x32_f16, three fp16 products per "
-                     f"fp32 product -> ceiling = dense fp16 peak {BF16_MFMA_PEAK_TF:.0f} / 3",
-        }.get(math, "fp32: v_mfma_f32_32x32x2_f32 dense peak")
-        roof = dict(bound="mfma", kernel=dom, achieved=round(ach, 2), peak=round(peak, 1),
-                    unit="TFLOP/s", frac=round(ach / peak, 4), traffic=traffic,
-                    traffic_unit="GB per launch", traffic_source=tsrc,
-                    samples_per_launch=nmax, avg_launch_ms=round(avg, 4),
-                    flop_per_sample=flop[dom], peak_basis=basis,
-                    frac_of_fp32_mfma_peak=round(ach / FP32_MFMA_PEAK_TF, 4))
-        d["share_of_step"] = d["total_ms"] / (ms * args.steps)
+        for k in ("mlp_fwd", "mlp_bwd_dgrad", "mlp_wgrad"):
+            if k in ks:
+                roofs[k] = kernel_roofline(k, timer.events[k], math, tj)
+        dom = max(roofs, key=lambda k: ks[k]["total_ms"])
+        roof = roofs[dom]
+        ks[dom]["share_of_step"] = ks[dom]["total_ms"] / (ms * args.steps)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
@@ -298,6 +315,7 @@ def main():
                                                 + (args.n_samples + args.n_importance)
                                                 * FLOP_TRAIN) / 1e12, 2),
             "roofline": roof,
+            "rooflines": roofs,
             "cpu_baseline": cpu,
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv
                             for kk, vv in v.items()} for k, v in ks.items()},
