@@ -33,6 +33,13 @@ ref = None
 for v in sys.argv[1].split(","):
     L = ctypes.CDLL(os.path.abspath(f"dev/libh3_{v}.so"))
     f, b, w = L.nr_mlp_fwd_h3, L.nr_mlp_bwd_h3, L.nr_wgrad_h3
+    # weights packed by the variant itself (its weight scale may differ)
+    L.nr_pack_h3.argtypes = [P, P, I64, P, P, P]
+    L.nr_pack_bwd_h3.argtypes = [P, P, I64, P, P]
+    m, hm = ops._maps3(0, 2)
+    mb = ops._map_bwd3(0, 2)
+    assert L.nr_pack_h3(flat.data_ptr(), m.data_ptr(), m.numel(), hm.data_ptr(), ph.data_ptr(), st) == 0
+    assert L.nr_pack_bwd_h3(flat.data_ptr(), mb.data_ptr(), mb.numel(), pbh.data_ptr(), st) == 0
     f.argtypes = [P, P, P, I64, I, P, I, I, P, P, P]
     b.argtypes = [P, P, P, P, P, I64, P, P]
     w.argtypes = [P, P, I64, P, P, P]

@@ -84,7 +84,8 @@ struct NrGrad {
 
 // keep x where mask bit b of word w is set, else +0 (ReLU backward)
 __device__ __forceinline__ float nr_mask_bit(float x, uint32_t w, int b) {
-    const uint32_t keep = 0u - ((w >> b) & 1u);
+    // signed one-bit field extract: 0 or all ones (v_bfe_i32 + v_and)
+    const uint32_t keep = (uint32_t)__builtin_amdgcn_sbfe((int)w, b, 1);
     return __uint_as_float(__float_as_uint(x) & keep);
 }
 

@@ -389,8 +389,8 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
     sa[0].init(tid); sa[1].init(tid);
     sb[0].init(tid); sb[1].init(tid);
     if constexpr (KA == SEG_HEAD) {     // rows 4..31 of the 4-row gradient image stay 0
-        for (int i = tid; i < 2 * 3 * 32 * kColB / 4; i += kThreads) {
-            const int b = i / (3 * 32 * kColB / 4), r = i % (3 * 32 * kColB / 4);
+        for (int i = tid; i < 2 * x3::kNP * 32 * kColB / 4; i += kThreads) {
+            const int b = i / (x3::kNP * 32 * kColB / 4), r = i % (x3::kNP * 32 * kColB / 4);
             const int p = r / (32 * kColB / 4), o = r % (32 * kColB / 4);
             reinterpret_cast<uint32_t*>(lds + b * kBufB + p * kPlane)[o] = 0u;
         }

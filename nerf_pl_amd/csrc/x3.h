@@ -73,7 +73,10 @@ typedef f16x2 p2;
 typedef _Float16 p1;
 constexpr int kNP = 2;                         // pieces per operand
 constexpr int kNProd = 3;                      // piece products per fp32 product
-constexpr int kWScale = 8;                     // packed weights carry 2^kWScale
+#ifndef NR_H3_WSCALE
+#define NR_H3_WSCALE 8
+#endif
+constexpr int kWScale = NR_H3_WSCALE;          // packed weights carry 2^kWScale
 #else
 typedef bf16x8 p8;
 typedef bf16x2 p2;
@@ -190,10 +193,22 @@ __device__ __forceinline__ void split2(float x0, float x1, bf16x2& hi, bf16x2& m
     const float s0 = r0 - bf16_as_f32(mid, 0), s1 = r1 - bf16_as_f32(mid, 1);
     lo = __builtin_convertvector((f32x2){s0, s1}, bf16x2);
 }
-// f16x3: hi = RN(x) (v_cvt_pk_f16_f32), lo = RN(x - hi); x - hi is exact in fp32
+// f16x3: hi = RN(x) (v_cvt_pk_f16_f32), lo = RN(x - hi); x - hi is exact in
+// fp32.  The residual is one v_fma_mix_f32 per value (-hi as an fp16 operand
+// times 1.0 plus x, a single exact rounding) instead of a conversion and a
+// subtraction: the split is VALU-issue-bound between MFMAs.
+#ifndef NR_H3_MIX
+#define NR_H3_MIX 1
+#endif
 __device__ __forceinline__ void split2h(float x0, float x1, f16x2& hi, f16x2& lo) {
     hi = __builtin_convertvector((f32x2){x0, x1}, f16x2);
+#if NR_H3_MIX
+    float r0, r1;
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r0) : "v"(hi), "v"(x0));
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r1) : "v"(hi), "v"(x1));
+#else
     const float r0 = x0 - (float)hi[0], r1 = x1 - (float)hi[1];
+#endif
     lo = __builtin_convertvector((f32x2){r0, r1}, f16x2);
 }
 

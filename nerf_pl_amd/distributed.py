@@ -16,10 +16,13 @@ import torch.distributed as dist
 class GradAllReducer:
     """Averages the ``.grad`` of ``params`` over the default process group.
 
-    Gradients are packed into one persistent flat buffer, all-reduced once and
-    scattered back.  Parameters without a gradient on every rank are treated as
-    zero (they contribute nothing to the sum), matching DDP's
-    ``find_unused_parameters`` behaviour for a fixed graph."""
+    Gradients are gathered into one persistent flat buffer (one batched
+    ``cat`` launch), all-reduced once (``AVG`` on RCCL; ``SUM`` and a scale on
+    gloo, which has no average) and scattered back with one batched foreach
+    copy -- a handful of launches per step instead of two per tensor.
+    Parameters without a gradient on every rank are treated as zero (they
+    contribute nothing to the sum), matching DDP's ``find_unused_parameters``
+    behaviour for a fixed graph."""
 
     def __init__(self, params, group=None):
         self.params = [p for p in params if p.requires_grad]
@@ -27,25 +30,22 @@ class GradAllReducer:
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.views = []
+        off = 0
+        for p in self.params:
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
 
     def __call__(self):
         world = dist.get_world_size(self.group)
-        off = 0
         for p in self.params:
-            k = p.numel()
             if p.grad is None:
-                self.flat[off:off + k].zero_()
-            else:
-                self.flat[off:off + k].copy_(p.grad.reshape(-1))
-            off += k
-        dist.all_reduce(self.flat, group=self.group)
-        self.flat.div_(world)
-        off = 0
-        for p in self.params:
-            k = p.numel()
-            g = self.flat[off:off + k].view_as(p)
-            if p.grad is None:
-                p.grad = g.clone()
-            else:
-                p.grad.copy_(g)
-            off += k
+                p.grad = torch.zeros_like(p)
+        grads = [p.grad for p in self.params]
+        torch.cat([g.reshape(-1) for g in grads], out=self.flat)
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(self.flat, group=self.group)
+            self.flat.div_(world)
+        torch._foreach_copy_(grads, self.views)

@@ -189,6 +189,9 @@ def main():
            "img": IMG, "train_views": 24, "test_views": 2, "draw_seed": args.draw_seed, "psnr": log, "loss": losses,
            "final_psnr": log[-1]["psnr"] if log else None,
            "threads": torch.get_num_threads() if args.impl == "reference" else None}
+    if args.impl == "ours":
+        from nerf_pl_amd import ops
+        out["mlp_arithmetic"] = ops.MATH
     path = args.out or os.path.join(REPO, "profiles", "r01", f"psnr_{args.impl}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
