@@ -77,3 +77,27 @@ def test_pe_pairing_covers_embedding_channels():
             a, b = m[g]
             if a >= 0 and b >= 0:
                 assert kind(a) == kind(b)
+
+
+def test_split_operand_maps_cover_every_weight_once():
+    """bf16x6 (3 pieces) and f16x3 (2 pieces) packed maps: every weight of the
+    forward appears once per piece; the transposed maps cover the weights the
+    dgrad chain needs, once per piece; sizes match the kernels' buffers."""
+    from nerf_pl_amd import packing
+    fwd_w = packing.build_fwd_map()
+    fwd_w = np.sort(fwd_w[fwd_w >= 0])
+    fwd_w = fwd_w[~np.isin(fwd_w, packing.build_fwd3_map(2)[1])]   # head entries
+    bwd_w = np.sort(packing.build_bwd_map())
+    for np_, fbytes, bbytes in ((3, 3575840, 3342336), (2, 2388000, 2228224)):
+        m, hm = packing.build_fwd3_map(np_)
+        assert m.size * 2 + packing.HEAD_BYTES == packing.fwd3_offsets(np_)[1] == fbytes
+        used = m[m >= 0]
+        assert set(np.unique(used & 3)) == set(range(np_))
+        for piece in range(np_):
+            w = np.sort(used[(used & 3) == piece] >> 2)
+            assert len(np.unique(w)) == len(w)
+            np.testing.assert_array_equal(w, fwd_w)
+        b = packing.build_bwd3_map(np_)
+        assert b.size * 2 == packing.bwd3_bytes(np_) == bbytes
+        for piece in range(np_):
+            np.testing.assert_array_equal(np.sort(b[(b & 3) == piece] >> 2), bwd_w)
