@@ -29,6 +29,14 @@ constexpr int kBufA = 256 * kCol;  // one operand region
 
 enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
 
+// interleave the workgroups of task pairs that read the same segment
+// (wgrad_launch).  Off: measured 3.52 vs 3.34 ms on the f16x3 fine pass -- the
+// pairs' equalised workgroup counts cost more than the MALL hits saved.
+#ifndef NR_WGRAD_PAIRS
+#define NR_WGRAD_PAIRS 0
+#endif
+constexpr bool kPairWg = NR_WGRAD_PAIRS;
+
 // flat parameter offsets, NeRF.named_parameters() order (packing.py param_offsets)
 struct POff {
     int w[12], b[12], fan[12];
@@ -71,6 +79,7 @@ struct WgTask {
     int64_t slab;        // slab offset (floats) of workgroup 0
     int id;              // task id: selects the gradient destination and the kernel shape
     int stat;            // f16x3: stats slot of the gradient operand (layout.h NR_STATS)
+    int pair;            // index (in WgArgs::task) of the task interleaved with this one, or -1
 };
 
 struct WgArgs {
@@ -251,8 +260,13 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     int t = 0;
 #pragma unroll 1
     while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
+    int c = blockIdx.x - a.wg_start[t];
+    if (a.task[t].pair >= 0) {   // interleaved pair (wgrad_launch): odd workgroups are the partner's
+        const int which = c & 1;
+        c >>= 1;
+        if (which) t = a.task[t].pair;
+    }
     const WgTask& T = a.task[t];
-    const int c = blockIdx.x - a.wg_start[t];
     const int b0 = (int)((int64_t)c * a.nb / T.G);
     const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
     float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
@@ -540,8 +554,13 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
     int t = 0;
 #pragma unroll 1
     while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
+    int c = blockIdx.x - a.wg_start[t];
+    if (a.task[t].pair >= 0) {   // interleaved pair (wgrad_launch): odd workgroups are the partner's
+        const int which = c & 1;
+        c >>= 1;
+        if (which) t = a.task[t].pair;
+    }
     const WgTask& T = a.task[t];
-    const int c = blockIdx.x - a.wg_start[t];
     const int b0 = (int)((int64_t)c * a.nb / T.G);
     const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
     float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
@@ -712,19 +731,45 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     static const int kStat[kTasks] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 8, 9, 9, 10, 10};
     static const long long tmask =
         getenv("NR_WGRAD_TASKMASK") ? strtoll(getenv("NR_WGRAD_TASKMASK"), nullptr, 0) : -1;
+    int64_t gt[kTasks];
+    int pos[kTasks];
     for (int k = 0; k < kTasks; ++k) {
         const int t = order[k];
         const int split = cost[t] >= heavy ? 1 : 3;
         int64_t g = split * ((kTargetWG * cost[t] + tot - 1) / tot);
-        g = std::max<int64_t>(1, std::min<int64_t>(g, nb));
-        if (!((tmask >> t) & 1)) g = 0;
+        gt[t] = std::max<int64_t>(1, std::min<int64_t>(g, nb));
+        if (!((tmask >> t) & 1)) gt[t] = 0;
+        pos[t] = k;
+    }
+    // Tasks that read the same saved segment run as interleaved pairs over the
+    // same block ranges: workgroup 2c of the first task's range is block range c
+    // of the first task, 2c+1 that of the second, so the two reads of the shared
+    // segment (DZ(4), H(7), dzdir: 2.5 KB/sample) land at about the same time and
+    // the second one can be served by the MALL instead of HBM (NR_WGRAD_PAIRS).
+    static const int kPairs[3][2] = {{4, 5}, {9, 12}, {10, 11}};
+    int second[kTasks];
+    bool absorbed[kTasks];
+    for (int t = 0; t < kTasks; ++t) { second[t] = -1; absorbed[t] = false; }
+    if (tmask == -1 && kPairWg) {
+        for (const auto& pr : kPairs) {
+            const int64_t g = std::max(gt[pr[0]], gt[pr[1]]);
+            gt[pr[0]] = gt[pr[1]] = g;
+            second[pr[0]] = pr[1];
+            absorbed[pr[1]] = true;
+        }
+    }
+    for (int k = 0; k < kTasks; ++k) {
+        const int t = order[k];
+        const int64_t g = gt[t];
         a.task[k] = tasks[t];
         a.task[k].id = t;
         a.task[k].stat = kStat[t];
         a.task[k].G = (int)g;
         a.task[k].slab = slab;
+        a.task[k].pair = second[t] >= 0 ? pos[second[t]] : -1;
         slab += g * (tasks[t].a.width * tasks[t].b.width + tasks[t].a.width);
-        a.wg_start[k + 1] = a.wg_start[k] + (int)g;
+        const int64_t range = absorbed[t] ? 0 : (second[t] >= 0 ? 2 * g : g);
+        a.wg_start[k + 1] = a.wg_start[k] + (int)range;
     }
     a.nb = (int)nb;
     a.n = (int)n;
