@@ -108,6 +108,10 @@ class _Composite(torch.autograd.Function):
         ctx.save_for_backward(raw, z, rays, noise if noise is not None else torch.empty(0))
         ctx.cfg = (noise is not None, noise_std, seed, stream, white_back)
         ctx.mark_non_differentiable(w)
+        # unused outputs (depth, opacity in the training loss) reach backward as
+        # None -- the kernel treats a null gradient as zero -- instead of as
+        # zero tensors autograd would fill with one launch each
+        ctx.set_materialize_grads(False)
         return rgb, depth, opac, w
 
     @staticmethod
