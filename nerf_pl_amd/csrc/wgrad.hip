@@ -20,7 +20,10 @@
 namespace {
 
 constexpr int kTasks = 14;
-constexpr int kTargetWG = 760;   // ~3 rounds of one workgroup per CU (short tail)
+#ifndef NR_WGRAD_TARGET_WG
+#define NR_WGRAD_TARGET_WG 760
+#endif
+constexpr int kTargetWG = NR_WGRAD_TARGET_WG;   // ~3 rounds of one workgroup per CU (short tail)
 constexpr int kThreads = 512;    // 8 waves: two per SIMD, so one wave's staging and
                                  // barrier time overlaps its partner's MFMAs
 constexpr int kCol = 36;         // LDS column stride (floats): [column][32 samples + 4 pad]
