@@ -32,13 +32,16 @@ constexpr int kBufA = 256 * kCol;  // one operand region
 
 enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
 
-// interleave the workgroups of task pairs that read the same segment
-// (wgrad_launch).  Off: measured 3.52 vs 3.34 ms on the f16x3 fine pass -- the
-// pairs' equalised workgroup counts cost more than the MALL hits saved.
-#ifndef NR_WGRAD_PAIRS
-#define NR_WGRAD_PAIRS 0
+// f16x3: the task pairs that read the same saved segment (wgrad_launch:
+// DZ(4), H(7), dz_dir) run fused -- one workgroup stages the shared segment
+// once and computes both outputs.  Runtime switch NR_WGRAD_FUSE=0 (host).
+constexpr bool kFuse = NR_F16;
+#ifndef NR_WG_PE_WM
+#define NR_WG_PE_WM 4            // wave grid rows of the fused PE output (256 x 64)
 #endif
-constexpr bool kPairWg = NR_WGRAD_PAIRS;
+#ifndef NR_WGRAD_FUSE_MASK
+#define NR_WGRAD_FUSE_MASK 7     // bit i: pair i of wgrad_launch's kFused (6: no spills, measured slower)
+#endif
 
 // flat parameter offsets, NeRF.named_parameters() order (packing.py param_offsets)
 struct POff {
@@ -82,7 +85,8 @@ struct WgTask {
     int64_t slab;        // slab offset (floats) of workgroup 0
     int id;              // task id: selects the gradient destination and the kernel shape
     int stat;            // f16x3: stats slot of the gradient operand (layout.h NR_STATS)
-    int pair;            // index (in WgArgs::task) of the task interleaved with this one, or -1
+    int fuse;            // f16x3: index (in WgArgs::task) of the task whose output this task's
+                         // workgroups also compute (same block ranges, its own slab), or -1
 };
 
 struct WgArgs {
@@ -263,12 +267,7 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     int t = 0;
 #pragma unroll 1
     while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
-    int c = blockIdx.x - a.wg_start[t];
-    if (a.task[t].pair >= 0) {   // interleaved pair (wgrad_launch): odd workgroups are the partner's
-        const int which = c & 1;
-        c >>= 1;
-        if (which) t = a.task[t].pair;
-    }
+    const int c = blockIdx.x - a.wg_start[t];
     const WgTask& T = a.task[t];
     const int b0 = (int)((int64_t)c * a.nb / T.G);
     const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
@@ -316,8 +315,10 @@ namespace w3 {
 constexpr int kColB = 48;                        // bytes per column (16 pieces + pad)
 constexpr int kPlane = 256 * kColB;              // one piece of one operand
 constexpr int kOpnd = x3::kNP * kPlane;          // one operand (all pieces)
-constexpr int kBufB = 2 * kOpnd;                 // one stage buffer (A + B)
-constexpr int kLds = 2 * kBufB;                  // double buffered: 147,456 B (bf16x6)
+constexpr int kXPlane = 64 * kColB;              // one piece of a fused task's extra operand
+constexpr int kXOpnd = kFuse ? x3::kNP * kXPlane : 0;
+constexpr int kBufB = 2 * kOpnd + kXOpnd;        // one stage buffer (A + B [+ X])
+constexpr int kLds = 2 * kBufB;                  // double buffered: 147,456 B (bf16x6), 110,592 B (f16x3)
 
 // The bf16x6 pipeline saves every segment in x3.h's N16 layout: float4 (F,
 // S, lane 16g + j) = columns 16F + 4g .. +3 of sample 16S + j (PE segments:
@@ -366,7 +367,8 @@ struct Stager {
     // split + store column e of this thread's chunk into an operand image
     // (values times sc, a power of two); samples >= nval become 0; adds the two
     // samples' unscaled sum (bias) to s
-    __device__ __forceinline__ void store_e(char* img, int nval, int e, float& s, float sc) {
+    __device__ __forceinline__ void store_e(char* img, int nval, int e, float& s, float sc,
+                                            int plane = kPlane) {
         if (!ALL && !act) return;
         const int j = 2 * jp;
         const float x0 = j < nval ? v0[e] : 0.f, x1 = j + 1 < nval ? v1[e] : 0.f;
@@ -376,21 +378,86 @@ struct Stager {
         x3::split_p2(x0 * sc, x1 * sc, pc);
         char* q = img + (c0 + e) * kColB + 4 * jp;
 #pragma unroll
-        for (int i = 0; i < x3::kNP; ++i) *reinterpret_cast<x3::p2*>(q + i * kPlane) = pc[i];
+        for (int i = 0; i < x3::kNP; ++i) *reinterpret_cast<x3::p2*>(q + i * plane) = pc[i];
     }
 };
+
+// A fused task's extra operand, staged thin: thread q < W * 8 loads one float2
+// (columns 2cp, 2cp + 1 of sample j of the half-block, q = 16 cp + j) -- 2
+// registers per set instead of Stager's 8 -- and writes single pieces.
+template <int KIND, int W>
+struct ThinStager {
+    static constexpr int Q = W * 8;            // float2 per half-block
+    bool act;
+    int j, c;                                  // sample, first column
+    x3::f32x2 v;
+    __device__ __forceinline__ void init(int tid) {
+        act = tid < Q;
+        const int q = act ? tid : 0;
+        j = q & 15; c = 2 * (q >> 4);
+    }
+    __device__ __forceinline__ void load(const float* base, int blk, int hb) {
+        size_t f;   // float offset of the pair
+        if constexpr (KIND == SEG_HEAD) f = 4 * ((size_t)blk * 32 + 16 * hb + j) + c;
+        else f = 4 * ((size_t)blk * (W / 8) * 64 + ((c >> 4) * 2 + hb) * 64 + 16 * ((c & 15) >> 2) + j) + (c & 3);
+        v = *reinterpret_cast<const x3::f32x2*>(base + f);
+    }
+    // split + store this thread's pair (times sc); s0/s1 += the unscaled values
+    __device__ __forceinline__ void store(char* img, int nval, float& s0, float& s1, float sc) {
+        if (!act) return;
+        const float x0 = j < nval ? v[0] : 0.f, x1 = j < nval ? v[1] : 0.f;
+        s0 += x0; s1 += x1;
+        x3::p2 pc[x3::kNP];
+        x3::split_p2(x0 * sc, x1 * sc, pc);
+        char* q = img + c * kColB + 2 * j;
+#pragma unroll
+        for (int i = 0; i < x3::kNP; ++i) {
+            *reinterpret_cast<x3::p1*>(q + i * kXPlane) = pc[i][0];
+            *reinterpret_cast<x3::p1*>(q + kColB + i * kXPlane) = pc[i][1];
+        }
+    }
+};
+
+// the pieces of one 32-column fragment at q (plane stride `plane`)
+__device__ __forceinline__ x3::Pieces frag(const char* q, int plane) {
+    x3::Pieces f;
+    f.hi = *reinterpret_cast<const x3::p8*>(q);
+#if NR_F16
+    f.lo = *reinterpret_cast<const x3::p8*>(q + plane);
+#else
+    f.mid = *reinterpret_cast<const x3::p8*>(q + plane);
+    f.lo = *reinterpret_cast<const x3::p8*>(q + 2 * plane);
+#endif
+    return f;
+}
 }  // namespace w3
 
-template <int KA, int WA, int KB, int WB, int WM, int WN>
+// One task's workgroup.  Optional fused extra operand X (kFuse, f16x3): XS = 0
+// X is a second input segment sharing the gradient operand A (extra output
+// M x XW), XS = 1 a second gradient segment sharing the input operand B (the
+// 4-row head: extra output XW x N); its XWM x XWN wave grid covers the extra
+// output (grids smaller than 8 waves are computed twice, written once) and the
+// result goes to the partner task's slab `xslab`.
+template <int KA, int WA, int KB, int WB, int WM, int WN, int XK = -1, int XW = 0, int XS = 0,
+          int XWM = 1, int XWN = 1>
 __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, int b0, int b1,
-                                            char* lds, float* __restrict__ slab) {
+                                            char* lds, float* __restrict__ slab,
+                                            float* __restrict__ xslab = nullptr) {
     using namespace w3;
     constexpr int MT = (WA / WM + 31) / 32, NT = (WB / WN + 31) / 32;
     constexpr int M = WA, N = WB;
+    constexpr bool HX = XK >= 0;
+    constexpr int XKK = HX ? XK : SEG_HEAD, XWW = HX ? XW : 4;
+    constexpr int XM = XS ? XW : M, XN = XS ? N : XW;              // extra output
+    constexpr int XMT = XS ? 1 : (M / XWM + 31) / 32;
+    constexpr int XNT = XS ? (N / XWN + 31) / 32 : (XWW / XWN + 31) / 32;
+    static_assert(!HX || (kFuse && XWM * XWN <= 8 && 8 % (XWM * XWN) == 0), "extra operand grid");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool active = wave < WM * WN;
     const int mi = wave / WN, ni = wave % WN;
     const int m0 = 32 * MT * mi, n0 = 32 * NT * ni;
+    const int xw = wave % (XWM * XWN);
+    const int xm0 = 32 * XMT * (xw / XWN), xn0 = 32 * XNT * (xw % XWN);
     const int h = lane >> 5, col = lane & 31;
 
     f32x16 acc[MT][NT];
@@ -398,32 +465,52 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
     for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x16{};
+    f32x16 xacc[HX ? XMT : 1][HX ? XNT : 1];
+    if constexpr (HX) {
+#pragma unroll
+        for (int i = 0; i < XMT; ++i)
+#pragma unroll
+            for (int j = 0; j < XNT; ++j) xacc[i][j] = f32x16{};
+    }
     float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+    float xbacc[2] = {0.f, 0.f};
 
     // two register sets per operand: the loads run two stages ahead
     Stager<KA, WA> sa[2];
     Stager<KB, WB> sb[2];
+    ThinStager<XKK, XWW> sx[2];
     sa[0].init(tid); sa[1].init(tid);
     sb[0].init(tid); sb[1].init(tid);
+    if constexpr (HX) { sx[0].init(tid); sx[1].init(tid); }
     if constexpr (KA == SEG_HEAD) {     // rows 4..31 of the 4-row gradient image stay 0
         for (int i = tid; i < 2 * x3::kNP * 32 * kColB / 4; i += kThreads) {
             const int b = i / (x3::kNP * 32 * kColB / 4), r = i % (x3::kNP * 32 * kColB / 4);
             const int p = r / (32 * kColB / 4), o = r % (32 * kColB / 4);
             reinterpret_cast<uint32_t*>(lds + b * kBufB + p * kPlane)[o] = 0u;
         }
-        __syncthreads();
     }
+    if constexpr (HX && XS == 1) {      // same for a head extra operand (whole X image)
+        for (int i = tid; i < 2 * kXOpnd / 4; i += kThreads) {
+            constexpr int kW = kXOpnd > 0 ? kXOpnd / 4 : 1;
+            const int b = i / kW, o = i % kW;
+            reinterpret_cast<uint32_t*>(lds + b * kBufB + 2 * kOpnd)[o] = 0u;
+        }
+    }
+    if constexpr (KA == SEG_HEAD || (HX && XS == 1)) __syncthreads();
     const int nst = 2 * (b1 - b0);      // half-block stages
     // stages past the end load a valid block and store zeros into a buffer
     // nobody reads again
     const int blast = b1 > b0 ? b1 - 1 : b0;
+    const float* xbase = HX ? (XS ? a.task[T.fuse].a.base : a.task[T.fuse].b.base) : nullptr;
     auto load = [&](int set, int st) {
         if (NR_W3_DBG == 2 && st > 1) return;
         const int blk = min(b0 + (st >> 1), blast), hb = st & 1;
         sa[set].load(T.a.base, blk, hb);
         sb[set].load(T.b.base, blk, hb);
+        if constexpr (HX) sx[set].load(xbase, blk, hb);
     };
     const float sca = task_scale(a, T);
+    const float scx = HX && XS ? task_scale(a, a.task[T.fuse]) : 1.f;
     auto store = [&](int set, int buf, int st) {
         const int nval = st < nst ? a.n - (b0 + (st >> 1)) * 32 - 16 * (st & 1) : 0;
         float sdummy = 0.f;
@@ -432,6 +519,7 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
             sa[set].store_e(lds + buf * kBufB, nval, e, bacc[e], sca);
             sb[set].store_e(lds + buf * kBufB + kOpnd, nval, e, sdummy, 1.f);
         }
+        if constexpr (HX) sx[set].store(lds + buf * kBufB + 2 * kOpnd, nval, xbacc[0], xbacc[1], scx);
     };
     // LDS-only barrier: keeps the prefetched global loads in flight
     auto barrier = [] {
@@ -443,33 +531,26 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
     // register set `set` into buffer buf ^ 1: the 8 store units (2 operands x
     // 4 columns) are spread between the row tiles' MFMAs so their VALU and
     // LDS-store work overlaps the MFMAs in flight instead of idling both waves
-    // of a SIMD at the same time
+    // of a SIMD at the same time; the extra operand's 4 units follow its MFMAs
     auto compute_store = [&](int buf, int set, int st_next) {
         const int nval = st_next < nst ? a.n - (b0 + (st_next >> 1)) * 32 - 16 * (st_next & 1) : 0;
         char* ia = lds + (buf ^ 1) * kBufB;
         char* ib = ia + kOpnd;
+        char* ix = ia + 2 * kOpnd;
         float sdummy = 0.f;
         auto unit = [&](int u) {
             if (NR_W3_DBG == 3) return;
             if (u < 4) sa[set].store_e(ia, nval, u, bacc[u], sca);
             else sb[set].store_e(ib, nval, u - 4, sdummy, 1.f);
         };
-        const char* la = lds + buf * kBufB + (m0 + col) * kColB + 16 * h;
-        const char* lb = lds + buf * kBufB + kOpnd + (n0 + col) * kColB + 16 * h;
+        const char* cur = lds + buf * kBufB;
+        const char* la = cur + (m0 + col) * kColB + 16 * h;
+        const char* lb = cur + kOpnd + (n0 + col) * kColB + 16 * h;
         const bool go = (WM * WN == 8 || active) && NR_W3_DBG != 1;
         x3::Pieces bp[NT];
         if (go) {
 #pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                const char* q = lb + 32 * j * kColB;
-                bp[j].hi = *reinterpret_cast<const x3::p8*>(q);
-#if NR_F16
-                bp[j].lo = *reinterpret_cast<const x3::p8*>(q + kPlane);
-#else
-                bp[j].mid = *reinterpret_cast<const x3::p8*>(q + kPlane);
-                bp[j].lo = *reinterpret_cast<const x3::p8*>(q + 2 * kPlane);
-#endif
-            }
+            for (int j = 0; j < NT; ++j) bp[j] = frag(lb + 32 * j * kColB, kPlane);
         }
         constexpr int UPT = (8 + MT - 1) / MT;   // store units per row tile
 #pragma unroll
@@ -490,6 +571,25 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
             for (int v = 0; v < UPT; ++v)
                 if (i * UPT + v < 8) unit(i * UPT + v);
         }
+        if constexpr (HX) {
+            // extra output: A rows from the A image (XS = 0) or the X image,
+            // B columns from the X image (XS = 0) or the B image
+            const char* xa = (XS ? cur + 2 * kOpnd : cur) + (xm0 + col) * kColB + 16 * h;
+            const char* xb = (XS ? cur + kOpnd : cur + 2 * kOpnd) + (xn0 + col) * kColB + 16 * h;
+            constexpr int PA = XS ? kXPlane : kPlane, PB = XS ? kPlane : kXPlane;
+            x3::Pieces xp[XNT];
+#pragma unroll
+            for (int j = 0; j < XNT; ++j) xp[j] = frag(xb + 32 * j * kColB, PB);
+#pragma unroll
+            for (int i = 0; i < XMT; ++i) {
+                x3::p8 ap[x3::kNP];
+#pragma unroll
+                for (int k = 0; k < x3::kNP; ++k)
+                    ap[k] = *reinterpret_cast<const x3::p8*>(xa + 32 * i * kColB + k * PA);
+                x3::mfma_xp_multi<XNT>(ap, xp, xacc[i]);
+            }
+            if (NR_W3_DBG != 3) sx[set].store(ix, nval, xbacc[0], xbacc[1], scx);
+        }
 #if NR_W3_SGB
         // interleave: per row tile, its fragment reads, then each MFMA followed
         // by two VALU ops of the store units, then the units' LDS stores
@@ -504,6 +604,15 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
                     __builtin_amdgcn_sched_group_barrier(0x002, NR_W3_SGB, 0);
                 }
                 __builtin_amdgcn_sched_group_barrier(0x200, x3::kNP * UPT, 0);
+            }
+            if constexpr (HX) {
+                __builtin_amdgcn_sched_group_barrier(0x100, x3::kNP * (XNT + XMT), 0);
+#pragma unroll
+                for (int r = 0; r < x3::kNProd * XNT * XMT; ++r) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, NR_W3_SGB, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x200, x3::kNP * 2, 0);
             }
         }
 #endif
@@ -532,11 +641,41 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
         bacc[e] += __shfl_xor(bacc[e], 2);
         bacc[e] += __shfl_xor(bacc[e], 4);
     }
+    if constexpr (HX && XS == 1) {      // over the 16 samples of each column pair
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int d = 1; d < 16; d <<= 1) xbacc[e] += __shfl_xor(xbacc[e], d);
+    }
     if (sa[0].act && sa[0].jp == 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int o = KA == SEG_HEAD ? e : Geo3<KA, WA>::col(sa[0].k, sa[0].h) + e;
-            if (o < M) slab[M * N + o] = bacc[e];
+            if (o < M) {
+                slab[M * N + o] = bacc[e];
+                if constexpr (HX && XS == 0) xslab[XM * XN + o] = bacc[e];   // shared gradient operand
+            }
+        }
+    }
+    if constexpr (HX && XS == 1) {      // the head extra operand is a gradient: its bias sums
+        if (sx[0].act && sx[0].j == 0) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                if (sx[0].c + e < XM) xslab[XM * XN + sx[0].c + e] = xbacc[e];
+        }
+    }
+    if constexpr (HX) {
+        if (wave < XWM * XWN) {
+#pragma unroll
+            for (int i = 0; i < XMT; ++i)
+#pragma unroll
+                for (int j = 0; j < XNT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int o = xm0 + 32 * i + nr_acc_row(r, h);
+                        const int c = xn0 + 32 * j + col;
+                        if (o < XM && c < XN) xslab[o * XN + c] = xacc[i][j][r];
+                    }
         }
     }
     if (!active) return;
@@ -557,16 +696,34 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
     int t = 0;
 #pragma unroll 1
     while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
-    int c = blockIdx.x - a.wg_start[t];
-    if (a.task[t].pair >= 0) {   // interleaved pair (wgrad_launch): odd workgroups are the partner's
-        const int which = c & 1;
-        c >>= 1;
-        if (which) t = a.task[t].pair;
-    }
+    const int c = blockIdx.x - a.wg_start[t];
     const WgTask& T = a.task[t];
     const int b0 = (int)((int64_t)c * a.nb / T.G);
     const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
     float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
+    const int fu = __builtin_amdgcn_readfirstlane(T.fuse);
+    if constexpr (kFuse) if (fu >= 0) {
+        const WgTask& P = a.task[fu];
+        float* xslab = a.slab + P.slab + (int64_t)c * (P.a.width * P.b.width + P.a.width);
+        switch (__builtin_amdgcn_readfirstlane(T.id)) {
+#if NR_WGRAD_FUSE_MASK & 1
+            case 5:    // DZ(4) x [H(3) | PE]: xyz_encoding_5 (skip layer)
+                wgrad3_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_PE, 64, 0, NR_WG_PE_WM, 8 / NR_WG_PE_WM>(
+                    a, T, b0, b1, lds, slab, xslab); break;
+#endif
+#if NR_WGRAD_FUSE_MASK & 2
+            case 9:    // [DZ(8) | head] x H(7): xyz_encoding_final and sigma
+                wgrad3_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_HEAD, 4, 1, 1, 8>(
+                    a, T, b0, b1, lds, slab, xslab); break;
+#endif
+#if NR_WGRAD_FUSE_MASK & 4
+            case 10:   // dz_dir x [feat | dir PE]: dir_encoding
+                wgrad3_body<SEG_ACC, 128, SEG_ACC, 256, 2, 4, SEG_DPE, 32, 0, 4, 1>(
+                    a, T, b0, b1, lds, slab, xslab); break;
+#endif
+        }
+        return;
+    }
     switch (__builtin_amdgcn_readfirstlane(T.id)) {
         case 0: case 4:
             wgrad3_body<SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
@@ -744,20 +901,23 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
         if (!((tmask >> t) & 1)) gt[t] = 0;
         pos[t] = k;
     }
-    // Tasks that read the same saved segment run as interleaved pairs over the
-    // same block ranges: workgroup 2c of the first task's range is block range c
-    // of the first task, 2c+1 that of the second, so the two reads of the shared
-    // segment (DZ(4), H(7), dzdir: 2.5 KB/sample) land at about the same time and
-    // the second one can be served by the MALL instead of HBM (NR_WGRAD_PAIRS).
-    static const int kPairs[3][2] = {{4, 5}, {9, 12}, {10, 11}};
-    int second[kTasks];
+    // f16x3: the tasks that read the same saved segment run fused (kFuse,
+    // wgrad3_body's extra operand): the primary's workgroups also compute the
+    // partner's output over the same block ranges into the partner's slabs, so
+    // DZ(4), H(7) and dz_dir (2.5 KB/sample) are read once.  The partner keeps
+    // its slabs and its reduction but launches no workgroups of its own.
+    static const int kFused[3][2] = {{5, 4}, {9, 12}, {10, 11}};   // {primary, partner}
+    static const bool fuse_on = !getenv("NR_WGRAD_FUSE") || atoi(getenv("NR_WGRAD_FUSE")) != 0;
+    int partner[kTasks];
     bool absorbed[kTasks];
-    for (int t = 0; t < kTasks; ++t) { second[t] = -1; absorbed[t] = false; }
-    if (tmask == -1 && kPairWg) {
-        for (const auto& pr : kPairs) {
-            const int64_t g = std::max(gt[pr[0]], gt[pr[1]]);
-            gt[pr[0]] = gt[pr[1]] = g;
-            second[pr[0]] = pr[1];
+    for (int t = 0; t < kTasks; ++t) { partner[t] = -1; absorbed[t] = false; }
+    if (kFuse && x3 && fuse_on && tmask == -1) {
+        for (int i = 0; i < 3; ++i) {
+            if (!((NR_WGRAD_FUSE_MASK >> i) & 1)) continue;
+            const auto& pr = kFused[i];
+            gt[pr[1]] = gt[pr[0]] = std::max<int64_t>(1, std::min<int64_t>(
+                (kTargetWG * (cost[pr[0]] + cost[pr[1]]) + tot - 1) / tot, nb));
+            partner[pr[0]] = pr[1];
             absorbed[pr[1]] = true;
         }
     }
@@ -769,10 +929,9 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
         a.task[k].stat = kStat[t];
         a.task[k].G = (int)g;
         a.task[k].slab = slab;
-        a.task[k].pair = second[t] >= 0 ? pos[second[t]] : -1;
+        a.task[k].fuse = partner[t] >= 0 ? pos[partner[t]] : -1;
         slab += g * (tasks[t].a.width * tasks[t].b.width + tasks[t].a.width);
-        const int64_t range = absorbed[t] ? 0 : (second[t] >= 0 ? 2 * g : g);
-        a.wg_start[k + 1] = a.wg_start[k] + (int)range;
+        a.wg_start[k + 1] = a.wg_start[k] + (absorbed[t] ? 0 : (int)g);
     }
     a.nb = (int)nb;
     a.n = (int)n;
