@@ -813,9 +813,16 @@ __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
     if (e >= sz) return;
     const int dst = e < nw ? wgrad_dest(T.id, e / N, e % N, a.x3) : wgrad_bias_dest(T.id, e - nw);
     if (dst < 0) return;
+    // 8 independent partial sums (fixed order: bitwise reproducible) keep 8
+    // slab loads in flight per thread instead of one dependent chain
     const float* p = a.slab + T.slab + e;
-    float s = 0.f;
-    for (int w = 0; w < T.G; ++w, p += sz) s += *p;
+    float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int w = 0;
+    for (; w + 8 <= T.G; w += 8, p += 8 * (int64_t)sz)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] += p[(int64_t)i * sz];
+    for (int i = 0; w < T.G; ++w, ++i, p += sz) q[i] += *p;
+    float s = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     if (e < nw) s /= task_scale(a, T);    // exact: a power of two
     grad[dst] = s;
 }
