@@ -123,11 +123,12 @@ def test_gradients_match_reference(case):
     assert n == 24 * len(models)
 
 
-@pytest.mark.parametrize("math,gscale,sboost", [
-    ("fp32", 1.0, 1.0), ("bf16x6", 1.0, 1.0), ("f16x3", 1.0, 1.0), ("f16x3", 1e-12, 1.0),
-    ("f16x3", 1e6, 1.0), ("f16x3", 1.0, 1e8), ("f16x3", 1.0, 1e-8), ("f16x3", 1.0, 1e12),
-    ("f16x3", 1e-18, 1.0)])
-def test_mlp_backward_matches_autograd(math, gscale, sboost, monkeypatch):
+@pytest.mark.parametrize("math,gscale,sboost,size", [
+    ("fp32", 1.0, 1.0, (23, 37)), ("bf16x6", 1.0, 1.0, (23, 37)), ("f16x3", 1.0, 1.0, (23, 37)),
+    ("f16x3", 1e-12, 1.0, (23, 37)), ("f16x3", 1e6, 1.0, (23, 37)), ("f16x3", 1.0, 1e8, (23, 37)),
+    ("f16x3", 1.0, 1e-8, (23, 37)), ("f16x3", 1.0, 1e12, (23, 37)), ("f16x3", 1e-18, 1.0, (23, 37)),
+    ("f16x3", 1.0, 1.0, (509, 61)), ("fp32", 1.0, 1.0, (509, 61))])
+def test_mlp_backward_matches_autograd(math, gscale, sboost, size, monkeypatch):
     """Full-gradient check (every parameter entry) of the fused MLP backward on
     random per-sample output gradients, against torch CPU autograd of the
     oracle MLP.  Samples with a pre-activation within 2e-6 of the ReLU kink
@@ -135,13 +136,16 @@ def test_mlp_backward_matches_autograd(math, gscale, sboost, monkeypatch):
     rare.  gscale multiplies the output gradient: f16x3 must keep the same
     relative accuracy for gradients far outside fp16's range (its power-of-two
     range scaling).  sboost multiplies the sigma gradient alone (the 1e10
-    last-sample delta of rendering.py:171 makes d sigma dwarf d rgb)."""
+    last-sample delta of rendering.py:171 makes d sigma dwarf d rgb).  The
+    (509, 61) size (31,049 samples, 971 blocks, ragged) runs the weight
+    gradient with many workgroups per task, so the f16x3 fused task pairs
+    (wgrad.hip kFused) split their block ranges the way a training step does."""
     from nerf_pl_amd import NeRF, ops
     from nerf_pl_amd.functions import mlp_apply
     monkeypatch.setattr(ops, "MATH", math)
     p = O.make_params(7, sigma_bias=0.4)
     g = torch.Generator().manual_seed(3)
-    n_rays, spr = 23, 37
+    n_rays, spr = size
     rays = torch.cat([torch.randn(n_rays, 3, generator=g) * 0.3,
                       torch.nn.functional.normalize(torch.randn(n_rays, 3, generator=g), dim=-1),
                       torch.full((n_rays, 1), 2.0), torch.full((n_rays, 1), 6.0)], 1)
