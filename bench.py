@@ -222,6 +222,9 @@ def main():
     models = [NeRF().to(dev), NeRF().to(dev)]
     emb = [Embedding(3, 10), Embedding(3, 4)]
     params = [p for m in models for p in m.parameters()]
+    # per-rank seed of the in-kernel Philox draws (PhiloxRNG takes each call's
+    # seed from the CPU generator): ranks draw independent perturb/noise/pdf streams
+    torch.manual_seed(4321 + rank)
     opt = FusedAdam(params, lr=5e-4, eps=1e-8)
     reducer = None
     if world > 1:

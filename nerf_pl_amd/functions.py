@@ -19,7 +19,11 @@ from ._lib import call, stream_of
 
 
 @functools.lru_cache(maxsize=None)
-def _wgrad_workspace(device_index: int) -> torch.Tensor:
+def _wgrad_workspace(device_index: int, stream: int) -> torch.Tensor:
+    """Split-K slab workspace of the weight gradient, one per (device, stream):
+    backward passes enqueued on different streams never share slabs.  The
+    size is the library's bound over every launch shape (~604 MB; the slabs a
+    launch uses depend only on the task list, not on n)."""
     from ._lib import lib
     nbytes = int(lib().nr_wgrad_workspace_bytes(0))
     return torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", device_index))
@@ -68,7 +72,7 @@ class _FusedMLP(torch.autograd.Function):
         call(ops.entry("nr_mlp_bwd", packed_b), packed_b.data_ptr(), ops.head_ptr(packed_f), out.data_ptr(),
              g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), stream_of(dev))
         gflat = torch.empty(packing.N_PARAMS, device=dev)
-        ws = _wgrad_workspace(dev.index)
+        ws = _wgrad_workspace(dev.index, int(stream_of(dev)))
         call(ops.entry("nr_wgrad", packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
              ws.data_ptr(), gflat.data_ptr(), stream_of(dev))
         if _DEBUG is not None:

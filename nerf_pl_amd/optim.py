@@ -64,4 +64,8 @@ class FusedAdam(torch.optim.Optimizer):
                          arr([c[2] for c in chunk]), arr([c[3] for c in chunk]), numel, k,
                          float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                          float(group["weight_decay"]), step, stream_of(dev))
+                # the kernel wrote through raw pointers: bump the version
+                # counters like torch's in-place Adam does, so autograd sees
+                # the modification and NeRF.packed() re-packs the new weights
+                torch.autograd.graph.increment_version([c[0] for c in items])
         return loss

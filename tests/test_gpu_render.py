@@ -197,19 +197,34 @@ def test_mlp_backward_matches_autograd(math, gscale, sboost, size, monkeypatch):
             f"{name}: err {err:.3g} scale {scale:.3g}"
 
 
-def test_training_steps_reduce_loss():
+@pytest.mark.parametrize("optim", ["torch_adam", "fused_adam"])
+def test_training_steps_reduce_loss(optim):
+    """30 steps on a learnable target with either optimiser.  FusedAdam writes
+    the parameters through raw pointers, so this also checks that the packed
+    weights the kernels read follow every optimiser step (a stale pack cache
+    would leave the output frozen at its step-0 value)."""
     from nerf_pl_amd import Embedding, NeRF, render_rays
+    from nerf_pl_amd.optim import FusedAdam
     from nerf_pl_amd.rays import blender_rays
     torch.manual_seed(0)
     rays = blender_rays(32, 1, near=2.0, far=6.0, device=DEV)[:512].contiguous()
     # a learnable target: a smooth colour field over ray directions
     target = (0.5 + 0.4 * torch.sin(3 * rays[:, 3:6])).contiguous()
     models = [NeRF().to(DEV), NeRF().to(DEV)]
-    opt = torch.optim.Adam([p for m in models for p in m.parameters()], lr=5e-4)
+    params = [p for m in models for p in m.parameters()]
+    opt = (torch.optim.Adam if optim == "torch_adam" else FusedAdam)(params, lr=5e-4)
+    emb = [Embedding(3, 10), Embedding(3, 4)]
+    probe = rays[:64].contiguous()
+
+    def probe_out():
+        with torch.no_grad():
+            return render_rays(models, emb, probe, 32, False, 0.0, 0.0, 32, 1024,
+                               False)["rgb_fine"].clone()
+
+    out0 = probe_out()
     losses = []
     for _ in range(30):
-        res = render_rays(models, [Embedding(3, 10), Embedding(3, 4)], rays, 32, False, 1.0, 1.0,
-                          32, 1024, False)
+        res = render_rays(models, emb, rays, 32, False, 1.0, 1.0, 32, 1024, False)
         loss = ((res["rgb_coarse"] - target) ** 2).mean() + ((res["rgb_fine"] - target) ** 2).mean()
         opt.zero_grad()
         loss.backward()
@@ -217,3 +232,30 @@ def test_training_steps_reduce_loss():
         losses.append(loss.item())
     assert np.isfinite(losses).all()
     assert losses[-1] < 0.7 * losses[0], losses
+    assert (probe_out() - out0).abs().max() > 1e-3
+    # the cached pack equals a fresh pack of the current parameters
+    from nerf_pl_amd import ops
+    for m in models:
+        pf, pb = m.packed(backward=True)
+        assert torch.equal(pf, ops.pack_fwd(m.flat_params()))
+        assert torch.equal(pb, ops.pack_bwd(m.flat_params()))
+
+
+def test_fused_adam_invalidates_pack_cache():
+    """One FusedAdam step must change the forward output of the next call."""
+    from nerf_pl_amd import NeRF
+    from nerf_pl_amd.functions import mlp_apply
+    from nerf_pl_amd.optim import FusedAdam
+    torch.manual_seed(0)
+    net = NeRF().to(DEV)
+    rays = torch.zeros(4, 8, device=DEV)
+    rays[:, 3] = 1.0
+    rays[:, 6], rays[:, 7] = 2.0, 6.0
+    z = torch.linspace(2.0, 6.0, 32, device=DEV).repeat(4)
+    out0 = mlp_apply(net, rays=rays, z=z, spr=32)
+    out0.sum().backward()
+    opt = FusedAdam(net.parameters(), lr=1e-2)
+    opt.step()
+    with torch.no_grad():
+        out1 = mlp_apply(net, rays=rays, z=z, spr=32)
+    assert (out1 - out0.detach()).abs().max() > 1e-4
