@@ -1,27 +1,46 @@
-"""Training-step throughput of the drop-in render_rays path on MI355X.
+"""Throughput of the drop-in render_rays path on MI355X.
 
-One step = one NeRFSystem.training_step of the reference (train.py:103-117)
-on synthetic Blender-lego 400x400 rays: B=4096 rays per rank generated on the
-device from the 100 camera poses of an orbit (nr_gen_rays; an epoch-shuffled
-permutation of all 16M pixels, like the reference's shuffled DataLoader over
-its ray buffer, with the target colours gathered in the same pass) ->
-render_rays (64 coarse + 128 fine, perturb=1, noise_std=1: opt.py defaults) ->
-MSE(coarse)+MSE(fine) -> backward -> [RCCL all-reduce of the 4.77 MB gradient
-when N>1] -> Adam(lr=5e-4, eps=1e-8) as one fused launch.
+Default workload (``--config cfg2``, BASELINE.json configs[1]): one step = one
+NeRFSystem.training_step of the reference (train.py:103-117) on synthetic
+Blender-lego 400x400 rays: B=4096 rays per rank generated on the device from
+the 100 camera poses of an orbit (nr_gen_rays; an epoch-shuffled permutation of
+all 16M pixels, like the reference's shuffled DataLoader over its ray buffer,
+with the target colours gathered in the same pass) -> render_rays (64 coarse +
+128 fine, perturb=1, noise_std=1: opt.py defaults) -> MSE(coarse)+MSE(fine) ->
+backward -> [RCCL all-reduce of the 4.77 MB gradient when N>1] -> Adam(lr=5e-4,
+eps=1e-8) as one fused launch.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+The other BASELINE.json configs are selectable (``--config``; the driver's
+default run is cfg2):
+
+* ``cfg3``: LLFF fern 504x378, forward-facing NDC rays (get_ndc_rays), 64 + 64
+  samples, batch 4096, training step as above (train.py with llff, 20 poses);
+* ``cfg4``: Blender lego 800x800, 64 + 128, batch 4096 per rank -- cfg2 at 800^2
+  (the 8-GPU data-parallel config);
+* ``cfg5``: shadow-mapping step of train_efficient_sm.py:143-199 at 128x128:
+  sigma-only render of 512 camera rays (64 + 64, noise 0, with gradients), the
+  whole 128x128 light image re-rendered every step (64 + 64 light importance,
+  no_grad: sample_light_depth_every=1), efficient_sm (shadow_method_2), MSE,
+  backward, Adam; camera batches in dataset order (its DataLoader has
+  shuffle=False), light image replicated on every rank;
+* ``eval``: eval.py's render of one 400x400 test view of cfg2's model
+  (test_time=True, perturb=0, noise_std=0, chunks of 32768 rays).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Prints ONE JSON line (rank 0).  ``value`` = rays/s over all ranks.  The
-``roofline`` object is for the dominant kernel, timed with HIP events around
-each of its launches inside the timed region; ``cpu_baseline`` times the CPU
-oracle (the reference algorithm restated in PyTorch-CPU, pinned to the
-reference by tests/golden) on a bounded sample on this host's cores.
+Prints ONE JSON line (rank 0).  ``value`` = rays/s over all ranks (camera rays
+for cfg5).  The ``roofline`` object is for the dominant kernel, timed with HIP
+events around each of its launches inside the timed region; ``cpu_baseline``
+times the CPU oracle (the reference algorithm restated in PyTorch-CPU, pinned
+to the reference by tests/golden) on a bounded sample of the same workload on
+this host's cores.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -40,29 +59,37 @@ SPLIT_PRODUCTS = {"bf16x6": 6, "f16x3": 3}
 HBM_PEAK_GBS = 8000.0
 # algorithmic FLOP per sample: forward, data-grad, weight-grad
 FLOP_FWD = 1_186_816
+FLOP_FWD_SIGMA = 982_528
 FLOP_DGRAD = 1_115_392
 FLOP_WGRAD = 1_186_816
 FLOP_TRAIN = FLOP_FWD + FLOP_DGRAD + FLOP_WGRAD   # 3,489,024
+# sigma-only graph trained (cfg5): forward + weight-grad of the sigma-only
+# layers, data-grad without the two PE inputs (layer 1 and layer 5's skip)
+FLOP_TRAIN_SIGMA = 2 * FLOP_FWD_SIGMA + 2 * (FLOP_FWD_SIGMA // 2 - 2 * 63 * 256)
 # weight gradient: algorithmic HBM bytes per sample (every saved segment read once)
 BYTES_WGRAD = 4 * (2528 + 2436)                     # 19,856
+KERNEL_FLOP = {"mlp_fwd": FLOP_FWD, "mlp_fwd_sigma": FLOP_FWD_SIGMA,
+               "mlp_bwd_dgrad": FLOP_DGRAD, "mlp_wgrad": FLOP_WGRAD}
+CONFIGS = ("cfg2", "cfg3", "cfg4", "cfg5", "eval")
 
 
-def kernel_roofline(k, events, math, traffic_json):
+def kernel_roofline(k, events, math_, traffic_json):
     """Roofline of one MLP kernel from its largest (fine-pass) launches, timed
     with HIP events on the stream it runs on.  The weight gradient streams every
-    saved segment once at 60 FLOP/B: HBM-bound (algorithmic bytes); the fused forward and data-gradient chains are MFMA-
-    bound (algorithmic FLOPs of the fp32 products)."""
+    saved segment once at 60 FLOP/B: HBM-bound (algorithmic bytes); the fused
+    forward and data-gradient chains are MFMA-bound (algorithmic FLOPs of the
+    fp32 products)."""
     big = [(s.elapsed_time(e), n) for s, e, n in events]
     nmax = max(n for _, n in big)
     durs = [t for t, n in big if n == nmax]
     avg = sum(durs) / len(durs)
-    flops = {"mlp_fwd": FLOP_FWD, "mlp_bwd_dgrad": FLOP_DGRAD, "mlp_wgrad": FLOP_WGRAD}[k]
+    flops = KERNEL_FLOP[k]
     tflops = flops * nmax / (avg * 1e-3) / 1e12
     traffic, tsrc = None, None
-    t = traffic_json.get(f"{math}/{k}") or traffic_json.get(k)
-    if t and int(t["samples"]) == nmax and t.get("arithmetic", math) == math:
+    t = traffic_json.get(f"{math_}/{k}") or traffic_json.get(k)
+    if t and int(t["samples"]) == nmax and t.get("arithmetic", math_) == math_:
         traffic = round(t["hbm_bytes"] / 1e9, 3)
-        tsrc = f"profiles/r01/traffic.json ({t['method']})"
+        tsrc = f"{t.get('file', 'profiles/r01/traffic.json')} ({t['method']})"
     common = dict(kernel=k, traffic=traffic, traffic_unit="GB per launch", traffic_source=tsrc,
                   samples_per_launch=nmax, avg_launch_ms=round(avg, 4))
     if k == "mlp_wgrad":
@@ -72,14 +99,14 @@ def kernel_roofline(k, events, math, traffic_json):
                     bytes_basis="every saved activation (2528 floats/sample) and gradient "
                                 "(2436 floats/sample) segment read once",
                     tflops_fp32_equiv=round(tflops, 2), **common)
-    np_ = SPLIT_PRODUCTS.get(math)
+    np_ = SPLIT_PRODUCTS.get(math_)
     peak = BF16_MFMA_PEAK_TF / np_ if np_ else FP32_MFMA_PEAK_TF
     basis = {
         "bf16x6": "bf16x6: fp32 FLOPs on v_mfma_f32_16x16x32_bf16, six bf16 products per "
                   f"fp32 product -> ceiling = dense bf16 peak {BF16_MFMA_PEAK_TF:.0f} / 6",
         "f16x3": "f16x3: fp32 FLOPs on v_mfma_f32_16x16x32_f16, three fp16 products per "
                  f"fp32 product -> ceiling = dense fp16 peak {BF16_MFMA_PEAK_TF:.0f} / 3",
-    }.get(math, "fp32: v_mfma_f32_32x32x2_f32 dense peak")
+    }.get(math_, "fp32: v_mfma_f32_32x32x2_f32 dense peak")
     return dict(bound="mfma", achieved=round(tflops, 2), peak=round(peak, 1), unit="TFLOP/s",
                 frac=round(tflops / peak, 4), flop_per_sample=flops, peak_basis=basis,
                 frac_of_fp32_mfma_peak=round(tflops / FP32_MFMA_PEAK_TF, 4), **common)
@@ -95,15 +122,24 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=4096, help="rays per rank per step")
-    ap.add_argument("--img", type=int, default=400)
+    ap.add_argument("--config", choices=CONFIGS, default="cfg2",
+                    help="BASELINE.json workload (cfg2 = the headline metric)")
+    ap.add_argument("--batch", type=int, default=None, help="rays per rank per step")
+    ap.add_argument("--img", type=int, default=None, help="image side (Blender configs)")
     ap.add_argument("--poses", type=int, default=100)
-    ap.add_argument("--n-samples", type=int, default=64)
-    ap.add_argument("--n-importance", type=int, default=128)
+    ap.add_argument("--n-samples", type=int, default=None)
+    ap.add_argument("--n-importance", type=int, default=None)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="budget of the CPU oracle sample (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    d = {"cfg2": (4096, 400, 64, 128), "cfg3": (4096, 504, 64, 64), "cfg4": (4096, 800, 64, 128),
+         "cfg5": (512, 128, 64, 64), "eval": (32768, 400, 64, 128)}[a.config]
+    a.batch = a.batch or d[0]
+    a.img = a.img or d[1]
+    a.n_samples = a.n_samples or d[2]
+    a.n_importance = a.n_importance if a.n_importance is not None else d[3]
+    return a
 
 
 class KernelTimer:
@@ -152,43 +188,307 @@ def install_timers(timer):
 
     _lib.call = timed_call
     ops.call = timed_call
+    import nerf_pl_amd.efficient_shadow_mapping as SM
     import nerf_pl_amd.functions as F
     import nerf_pl_amd.optim as OP
-    F.call = timed_call
-    OP.call = timed_call
+    import nerf_pl_amd.rays as R
+    for m in (F, OP, SM, R):
+        m.call = timed_call
 
 
-def cpu_baseline(args, budget_s):
-    """Oracle (reference algorithm, PyTorch CPU) training step on a bounded
-    sample of the same workload: B_cpu rays, same sample counts."""
+# ---------------------------------------------------------------------------
+# CPU baselines: the oracle (reference algorithm, PyTorch CPU) on a bounded
+# sample of the same workload, on this host's cores
+# ---------------------------------------------------------------------------
+def _cpu_threads():
+    t = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(t)
+    return t
+
+
+def _timed_loop(fn, budget_s, min_iters=2):
+    n, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and n >= min_iters:
+            return n, el
+
+
+def cpu_train(args, budget_s, rays_all, label):
+    """Oracle training steps (render_rays fwd + bwd + Adam) on b=256-ray batches."""
     from oracle import nerf_oracle as O
-    from nerf_pl_amd.rays import blender_rays
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    threads = _cpu_threads()
     torch.manual_seed(0)
-    rays_all = blender_rays(args.img, 1)
     b = 256
     params = [{k: v.requires_grad_(True) for k, v in O.make_params(s).items()} for s in (1, 2)]
     opt = torch.optim.Adam([p for d in params for p in d.values()], lr=5e-4)
-    n_rays, t0, steps = 0, time.perf_counter(), 0
-    while True:
+
+    def step():
         idx = torch.randint(0, rays_all.shape[0], (b,))
-        rays = rays_all[idx]
-        tgt = torch.rand(b, 3)
-        res = O.render_rays(params, rays, args.n_samples, False, 1.0, 1.0, args.n_importance,
-                            32768, False)
-        loss = O.mse_loss(res, tgt)
+        res = O.render_rays(params, rays_all[idx], args.n_samples, False, 1.0, 1.0,
+                            args.n_importance, 32768, False)
+        loss = O.mse_loss(res, torch.rand(b, 3))
         opt.zero_grad()
         loss.backward()
         opt.step()
-        n_rays += b
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s and steps >= 2:
-            break
-    return dict(value=n_rays / el, unit="rays/s", cores=threads, kind="port",
-                sample=f"{steps} oracle training steps x {b} rays (64+128 samples, fwd+bwd+Adam) "
-                       f"in {el:.1f} s, torch CPU {threads} threads")
+    n, el = _timed_loop(step, budget_s)
+    return dict(value=n * b / el, unit="rays/s", cores=threads, kind="port",
+                sample=f"{n} oracle training steps x {b} rays ({label}, {args.n_samples}+"
+                       f"{args.n_importance} samples, fwd+bwd+Adam) in {el:.1f} s, torch CPU "
+                       f"{threads} threads")
+
+
+def cpu_eval(args, budget_s, rays_all):
+    from oracle import nerf_oracle as O
+    threads = _cpu_threads()
+    b = 1024
+    params = [O.make_params(s) for s in (1, 2)]
+    pos = [0]
+
+    def step():
+        rays = rays_all[pos[0]:pos[0] + b]
+        pos[0] = (pos[0] + b) % (rays_all.shape[0] - b)
+        with torch.no_grad():
+            O.render_rays(params, rays, args.n_samples, False, 0.0, 0.0, args.n_importance,
+                          32768, False, True)
+    n, el = _timed_loop(step, budget_s)
+    return dict(value=n * b / el, unit="rays/s", cores=threads, kind="port",
+                sample=f"{n} oracle test_time renders x {b} rays ({args.n_samples}+"
+                       f"{args.n_importance}) in {el:.1f} s, torch CPU {threads} threads")
+
+
+def cpu_shadow(args, budget_s, scene):
+    """cfg5 on the CPU oracle, timed in two parts on bounded samples -- the
+    camera part (sigma-only render of b rays + efficient_sm against a light
+    map + MSE backward + Adam) and the no_grad light render (per ray) -- then
+    combined into the step rate of the full workload (512 camera rays + the
+    whole light image per step)."""
+    from oracle import nerf_oracle as O
+    from oracle import shadow_oracle as SO
+    threads = _cpu_threads()
+    torch.manual_seed(0)
+    params = [{k: v.requires_grad_(True) for k, v in O.make_params(s).items()} for s in (1, 2)]
+    opt = torch.optim.Adam([p for d in params for p in d.values()], lr=5e-4)
+    S, I, wh = args.n_samples, args.n_importance, args.img
+    lrays = scene["light_rays"].cpu()
+    lpix = scene["light_pixels"].cpu()
+    leye, lcam = scene["light_eye"].cpu(), scene["light_cam"].cpu()
+    bl = 256
+    light_map = {"depth_coarse": torch.full((wh * wh,), 4.0), "depth_fine": torch.full((wh * wh,), 4.0)}
+
+    def light_part():
+        with torch.no_grad():
+            SO.render_rays(params, lrays[:bl], S, False, 1.0, 0.0, I, 32768, False)
+    b = 64
+
+    def cam_part():
+        sel = torch.arange(b)
+        rays = scene["rays_all"][sel].cpu()
+        ppc = {"eye_pos": scene["eyes"][0].cpu().expand(b, 3),
+               "camera": scene["mats"][0].cpu().expand(b, 3, 3)}
+        res = SO.render_rays(params, rays, S, False, 1.0, 0.0, I, 32768, False)
+        out = SO.efficient_sm(scene["pixels"][sel].cpu(), lpix, res, light_map, ppc, leye, lcam,
+                              (wh, wh), I > 0, I > 0, "shadow_method_2")
+        tgt = torch.rand(b, 3)
+        loss = torch.mean((out["rgb_coarse"] - tgt) ** 2) + torch.mean((out["rgb_fine"] - tgt) ** 2)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    nc, elc = _timed_loop(cam_part, budget_s / 2)
+    nl, ell = _timed_loop(light_part, budget_s / 2)
+    t_cam, t_light = elc / (nc * b), ell / (nl * bl)
+    t_step = args.batch * t_cam + wh * wh * t_light
+    return dict(value=args.batch / t_step, unit="camera rays/s", cores=threads, kind="port",
+                sample=f"camera part {nc} x {b} rays in {elc:.1f} s, light render {nl} x {bl} rays "
+                       f"in {ell:.1f} s (oracle, torch CPU {threads} threads), combined per step "
+                       f"as {args.batch} camera rays + {wh * wh} light rays")
+
+
+# ---------------------------------------------------------------------------
+# workloads
+# ---------------------------------------------------------------------------
+def _models(dev):
+    from nerf_pl_amd import Embedding, NeRF
+    torch.manual_seed(0)                      # identical initial weights on every rank
+    models = [NeRF().to(dev), NeRF().to(dev)]
+    return models, [Embedding(3, 10), Embedding(3, 4)]
+
+
+def wl_nerf_train(args, dev, rank, ndc):
+    """cfg2 / cfg4 (Blender) and cfg3 (LLFF NDC) training steps."""
+    from nerf_pl_amd import render_rays
+    from nerf_pl_amd.rays import RaySampler, blender_focal, pose_spherical
+    torch.manual_seed(1234 + rank)
+    if ndc:
+        W, H, focal, near, far = 504, 378, 407.0, 0.0, 1.0
+        poses = []
+        for k in range(20):                   # forward-facing: small translations, no rotation
+            ang = 2 * math.pi * k / 20
+            c2w = torch.eye(4)[:3].clone()
+            c2w[:, 3] = torch.tensor([0.1 * math.cos(ang), 0.1 * math.sin(ang), 0.0])
+            poses.append(c2w)
+        poses = torch.stack(poses).to(dev)
+    else:
+        W = H = args.img
+        focal, near, far = blender_focal(W), 1.0, 200.0   # datasets/blender.py:40-41
+        poses = torch.stack([pose_spherical(-180.0 + 360.0 * k / args.poses, -30.0, 4.0)
+                             for k in range(args.poses)]).to(dev)
+    pool_rgb = torch.rand(poses.shape[0] * H * W, 3, device=dev)
+    sampler = RaySampler(poses, H, W, focal, near, far, rgb_pool=pool_rgb, ndc=ndc,
+                         seed=99 + rank)
+    models, emb = _models(dev)
+    torch.manual_seed(4321 + rank)            # per-rank seeds of the in-kernel Philox draws
+    S, I = args.n_samples, args.n_importance
+
+    def step():
+        rays, rgbs = sampler.next(args.batch)
+        res = render_rays(models, emb, rays, S, False, 1.0, 1.0, I, 32768, False)
+        return torch.mean((res["rgb_coarse"] - rgbs) ** 2) + torch.mean((res["rgb_fine"] - rgbs) ** 2)
+
+    if ndc:
+        name = "cfg3"
+        metric = f"rays/sec ({S}c+{I}f) LLFF fern 504x378 NDC training step"
+        work = (f"cfg3: LLFF fern 504x378 (20 forward-facing poses, focal 407), NDC rays "
+                f"(near/far 0/1), {S} coarse + {I} fine, batch {args.batch} rays/rank, "
+                "perturb=1, noise_std=1, MSE coarse+fine, Adam lr 5e-4")
+        data = "synthetic (forward-facing NDC rays generated on device per batch, random target colours)"
+    else:
+        name = "cfg2" if args.img == 400 else f"cfg4" if args.img == 800 else f"blender{args.img}"
+        metric = f"rays/sec ({S}c+{I}f) Blender-lego {W}^2 training step"
+        work = (f"{name}: Blender lego {W}x{W}, {S} coarse + {I} fine, batch {args.batch} "
+                "rays/rank, perturb=1, noise_std=1, MSE coarse+fine, Adam lr 5e-4")
+        data = (f"synthetic (Blender-lego {W}x{W}, {args.poses}-pose camera orbit, rays generated "
+                "on device per batch, random target colours, seeded default-init NeRF coarse+fine)")
+
+    def cpu(budget):
+        if ndc:
+            from nerf_pl_amd.rays import llff_ndc_rays
+            rays_all = llff_ndc_rays(504, 378, 4, 407.0)
+        else:
+            from nerf_pl_amd.rays import blender_rays
+            rays_all = blender_rays(W, 1)
+        return cpu_train(args, budget, rays_all, name)
+
+    return dict(name=name, metric=metric, workload=work, data=data, step=step, train=True,
+                models=models, rays_per_step=args.batch, samples_per_ray=S + I,
+                flop_per_ray=S * FLOP_TRAIN + (S + I) * FLOP_TRAIN, cpu=cpu)
+
+
+def wl_eval(args, dev, rank):
+    """eval.py:58-86 -- one test view rendered in chunks (test_time=True)."""
+    from nerf_pl_amd import render_rays
+    from nerf_pl_amd.rays import blender_focal, generate_rays, pose_spherical
+    W = args.img
+    models, emb = _models(dev)
+    for m in models:
+        m.requires_grad_(False)
+    S, I = args.n_samples, args.n_importance
+    poses = torch.stack([pose_spherical(-180.0 + 360.0 * k / 8, -30.0, 4.0) for k in range(8)]).to(dev)
+    views = [generate_rays(poses[k:k + 1], W, W, blender_focal(W), 1.0, 200.0)
+             for k in range(poses.shape[0])]
+    it = [rank]
+
+    def step():
+        rays = views[it[0] % len(views)]
+        it[0] += 1
+        with torch.no_grad():
+            for i in range(0, rays.shape[0], args.batch):
+                render_rays(models, emb, rays[i:i + args.batch], S, False, 0.0, 0.0, I, 32768,
+                            False, True)
+        return None
+
+    def cpu(budget):
+        from nerf_pl_amd.rays import blender_rays
+        return cpu_eval(args, budget, blender_rays(W, 1))
+
+    return dict(name="eval", metric=f"rays/sec ({S}c+{I}f) Blender-lego {W}^2 test-view render",
+                workload=f"eval: eval.py render of one {W}x{W} Blender-lego test view per step "
+                         f"({W * W} rays, test_time=True: sigma-only coarse {S}, full fine "
+                         f"{S + I}; perturb=0, noise_std=0, chunks of {args.batch} rays)",
+                data="synthetic (Blender-lego camera orbit, seeded default-init NeRF coarse+fine)",
+                step=step, train=False, models=models, rays_per_step=W * W,
+                samples_per_ray=S + I, flop_per_ray=S * FLOP_FWD_SIGMA + (S + I) * FLOP_FWD,
+                cpu=cpu)
+
+
+def shadow_scene(wh, n_poses, dev):
+    """datasets/blender_efficient_sm.py-style scene (as tests/golden/make_golden_shadow.py):
+    a light camera on the sphere, n_poses camera poses, [i+.5, j+.5, 1] pixels."""
+    from nerf_pl_amd.camera import Camera
+    from nerf_pl_amd.rays import LEGO_CAMERA_ANGLE_X, blender_focal, generate_rays, pose_spherical
+    focal = blender_focal(wh)
+    hfov = LEGO_CAMERA_ANGLE_X * 180. / math.pi
+    l2w = pose_spherical(35.0, -55.0, 4.0)
+    light = Camera(hfov, (wh, wh))
+    light.set_pose_using_blender_matrix(l2w, False)
+    jj, ii = torch.meshgrid(torch.arange(wh), torch.arange(wh), indexing="ij")
+    pixels = torch.stack([ii + 0.5, jj + 0.5, torch.ones_like(ii, dtype=torch.float32)], -1)
+    pixels = pixels.reshape(-1, 3).float().to(dev)
+    c2ws, eyes, mats = [], [], []
+    for k in range(n_poses):
+        c2w = pose_spherical(-180.0 + 360.0 * k / n_poses, -30.0, 4.0)
+        cam = Camera(hfov, (wh, wh))
+        cam.set_pose_using_blender_matrix(c2w, False)
+        c2ws.append(c2w)
+        eyes.append(cam.eye_pos)
+        mats.append(cam.camera)
+    c2ws = torch.stack(c2ws).to(dev)
+    return dict(light_rays=generate_rays(l2w.reshape(1, 3, 4).to(dev), wh, wh, focal, 1.0, 200.0),
+                light_pixels=pixels, light_eye=light.eye_pos.float(), light_cam=light.camera.float(),
+                light=light, c2ws=c2ws, eyes=torch.stack(eyes).float().to(dev),
+                mats=torch.stack(mats).float().to(dev), pixels=pixels, focal=focal,
+                rays_all=generate_rays(c2ws[:1], wh, wh, focal, 1.0, 200.0))
+
+
+def wl_shadow(args, dev, rank):
+    """cfg5: train_efficient_sm.py:143-199 (sample_light_depth_every=1)."""
+    from nerf_pl_amd import rendering_shadows as RS
+    from nerf_pl_amd.rays import generate_rays
+    wh, S, I, B = args.img, args.n_samples, args.n_importance, args.batch
+    scene = shadow_scene(wh, args.poses, dev)
+    models, emb = _models(dev)
+    torch.manual_seed(4321 + rank)
+    hw = wh * wh
+    total = args.poses * hw
+    pos = [(rank * B) % total]
+    tgt_pool = torch.rand(total, 3, device=dev)
+    light_ppc = {"eye_pos": scene["light_eye"], "camera": scene["light_cam"]}
+
+    def step():
+        # dataset order (shuffle=False): B consecutive pixels of one view
+        sel = torch.arange(pos[0], pos[0] + B, device=dev)
+        pos[0] = (pos[0] + B * max(1, dist.get_world_size() if dist.is_initialized() else 1)) % total
+        rays = generate_rays(scene["c2ws"], wh, wh, scene["focal"], 1.0, 200.0, sel)
+        pose = sel // hw
+        ppc = {"eye_pos": scene["eyes"][pose], "camera": scene["mats"][pose]}
+        cam = RS.render_rays(models, emb, rays, S, False, 1.0, 0.0, I, 32768, False)
+        with torch.no_grad():
+            light = RS.render_rays(models, emb, scene["light_rays"], S, False, 1.0, 0.0, I, 32768,
+                                   False, were_gradients_computed=False)
+        out = RS.efficient_sm(scene["pixels"][sel % hw], scene["light_pixels"], cam, light, ppc,
+                              light_ppc, (wh, wh), I > 0, I > 0, "shadow_method_2")
+        tgt = tgt_pool[sel]
+        loss = torch.mean((out["rgb_coarse"] - tgt) ** 2)
+        if "rgb_fine" in out:
+            loss = loss + torch.mean((out["rgb_fine"] - tgt) ** 2)
+        return loss
+
+    return dict(name="cfg5",
+                metric=f"camera rays/sec shadow-mapping step ({S}c+{I}f, {wh}^2 light image "
+                       "re-rendered per step)",
+                workload=f"cfg5: train_efficient_sm.py step at {wh}x{wh}: sigma-only render of "
+                         f"{B} camera rays/rank ({S}+{I}, noise_std=0, with gradients) + no_grad "
+                         f"render of the {hw}-ray light image ({S}+{I}) + efficient_sm "
+                         "(shadow_method_2, per-pose runs) + MSE + backward + Adam lr 5e-4",
+                data=f"synthetic ({args.poses}-pose camera orbit + one light camera, rays "
+                     "generated on device, random targets, seeded default-init NeRF pair)",
+                step=step, train=True, models=models, rays_per_step=B,
+                samples_per_ray=S + I,
+                flop_per_ray=(S + (S + I)) * FLOP_TRAIN_SIGMA
+                + hw / B * (S * FLOP_FWD_SIGMA + (S + I) * FLOP_FWD_SIGMA),
+                cpu=lambda budget: cpu_shadow(args, budget, scene))
 
 
 def main():
@@ -202,45 +502,35 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from nerf_pl_amd import Embedding, NeRF, render_rays
     from nerf_pl_amd.optim import FusedAdam
-    from nerf_pl_amd.rays import RaySampler, blender_focal, pose_spherical
 
     timer = KernelTimer()
     if not args.no_kernel_timing:
         install_timers(timer)
 
-    # camera poses + target images resident in HBM (datasets/blender.py); rays
-    # are generated per batch (near/far 1/200: datasets/blender.py:40-41)
-    torch.manual_seed(1234 + rank)
-    poses = torch.stack([pose_spherical(-180.0 + 360.0 * k / args.poses, -30.0, 4.0)
-                         for k in range(args.poses)]).to(dev)
-    pool_rgb = torch.rand(args.poses * args.img * args.img, 3, device=dev)
-    sampler = RaySampler(poses, args.img, args.img, blender_focal(args.img), 1.0, 200.0,
-                         rgb_pool=pool_rgb, seed=99 + rank)
-    torch.manual_seed(0)                      # identical initial weights on every rank
-    models = [NeRF().to(dev), NeRF().to(dev)]
-    emb = [Embedding(3, 10), Embedding(3, 4)]
-    params = [p for m in models for p in m.parameters()]
-    # per-rank seed of the in-kernel Philox draws (PhiloxRNG takes each call's
-    # seed from the CPU generator): ranks draw independent perturb/noise/pdf streams
-    torch.manual_seed(4321 + rank)
-    opt = FusedAdam(params, lr=5e-4, eps=1e-8)
-    reducer = None
-    if world > 1:
-        from nerf_pl_amd.distributed import GradAllReducer
-        reducer = GradAllReducer(params)
+    if args.config == "eval":
+        wl = wl_eval(args, dev, rank)
+    elif args.config == "cfg5":
+        wl = wl_shadow(args, dev, rank)
+    else:
+        wl = wl_nerf_train(args, dev, rank, ndc=args.config == "cfg3")
+
+    opt, reducer = None, None
+    if wl["train"]:
+        params = [p for m in wl["models"] for p in m.parameters()]
+        opt = FusedAdam(params, lr=5e-4, eps=1e-8)
+        if world > 1:
+            from nerf_pl_amd.distributed import GradAllReducer
+            reducer = GradAllReducer(params)
 
     def step():
-        rays, rgbs = sampler.next(args.batch)
-        res = render_rays(models, emb, rays, args.n_samples, False, 1.0, 1.0,
-                          args.n_importance, 32768, False)
-        loss = torch.mean((res["rgb_coarse"] - rgbs) ** 2) + torch.mean((res["rgb_fine"] - rgbs) ** 2)
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        if reducer is not None:
-            reducer()            # one RCCL all-reduce of the 4.77 MB gradient
-        opt.step()
+        loss = wl["step"]()
+        if opt is not None:
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            if reducer is not None:
+                reducer()            # one RCCL all-reduce of the 4.77 MB gradient
+            opt.step()
         return loss
 
     for _ in range(args.warmup):
@@ -262,30 +552,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
     ms = el / args.steps * 1e3
-    rays_per_s = args.batch * world * args.steps / el
+    rays_per_s = wl["rays_per_step"] * world * args.steps / el
 
     ks = timer.summary()
     roof, roofs = None, {}
     if ks:
-        math = _math()
+        math_ = _math()
         tj = {}
-        tf = os.path.join(REPO, "profiles", "r01", "traffic.json")
-        if os.path.exists(tf):
-            tj = json.load(open(tf))
-        for k in ("mlp_fwd", "mlp_bwd_dgrad", "mlp_wgrad"):
+        for rel in ("profiles/r02/traffic.json", "profiles/r01/traffic.json"):
+            tf = os.path.join(REPO, rel)
+            if os.path.exists(tf):
+                tj = {k: dict(v, file=rel) for k, v in json.load(open(tf)).items()
+                      if isinstance(v, dict)}
+                break
+        for k in KERNEL_FLOP:
             if k in ks:
-                roofs[k] = kernel_roofline(k, timer.events[k], math, tj)
+                roofs[k] = kernel_roofline(k, timer.events[k], math_, tj)
         dom = max(roofs, key=lambda k: ks[k]["total_ms"])
         roof = roofs[dom]
         ks[dom]["share_of_step"] = ks[dom]["total_ms"] / (ms * args.steps)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
-        cpu = cpu_baseline(args, args.cpu_baseline_seconds)
+        cpu = wl["cpu"](args.cpu_baseline_seconds)
 
     if rank == 0:
         line = {
-            "metric": "rays/sec (64c+128f) Blender-lego 400^2 training step",
+            "metric": wl["metric"],
             "value": round(rays_per_s, 1),
             "unit": "rays/s",
             "n_gpus": world,
@@ -305,24 +598,18 @@ def main():
                          "scheme; fp32 inputs/outputs, parity-tested against the reference "
                          "at 1e-4)",
             }.get(_math(), "fp32"),
-            "data": "synthetic (Blender-lego 400x400, 100-pose camera orbit, rays generated "
-                    "on device per batch, random target colours, seeded default-init NeRF "
-                    "coarse+fine)",
-            "config": {"workload": "cfg2: Blender lego 400x400, 64 coarse + 128 fine, "
-                                   f"batch {args.batch} rays/rank, perturb=1, noise_std=1, "
-                                   "MSE coarse+fine, Adam lr 5e-4",
-                       "global_batch": args.batch * world,
-                       "samples_per_ray": args.n_samples + args.n_importance,
-                       "parallelism": f"dp{world}"},
-            "model_tflops": round(rays_per_s * (args.n_samples * FLOP_TRAIN
-                                                + (args.n_samples + args.n_importance)
-                                                * FLOP_TRAIN) / 1e12, 2),
+            "data": wl["data"],
+            "config": {"workload": wl["workload"],
+                       "global_batch": wl["rays_per_step"] * world,
+                       "samples_per_ray": wl["samples_per_ray"],
+                       "parallelism": f"dp{world}" if wl["train"] else f"replicas{world}"},
+            "model_tflops": round(rays_per_s * wl["flop_per_ray"] / 1e12, 2),
             "roofline": roof,
             "rooflines": roofs,
             "cpu_baseline": cpu,
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv
                             for kk, vv in v.items()} for k, v in ks.items()},
-            "final_loss": round(loss.item(), 5),
+            "final_loss": round(loss.item(), 5) if loss is not None else None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

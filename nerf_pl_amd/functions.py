@@ -19,7 +19,7 @@ from ._lib import call, stream_of
 
 
 @functools.lru_cache(maxsize=None)
-def _wgrad_workspace(device_index: int, stream: int) -> torch.Tensor:
+def _wgrad_workspace(device_index: int, stream: int = 0) -> torch.Tensor:
     """Split-K slab workspace of the weight gradient, one per (device, stream):
     backward passes enqueued on different streams never share slabs.  The
     size is the library's bound over every launch shape (~604 MB; the slabs a
