@@ -55,7 +55,7 @@ FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: fp32 matrix (= vector)
 BF16_MFMA_PEAK_TF = 16 * FP32_MFMA_PEAK_TF   # dense bf16 MFMA (1/16 ratio, same guide)
 # split-operand arithmetics: every fp32 product costs six bf16 (bf16x6) or three
 # fp16 (f16x3; dense fp16 = dense bf16 rate) MFMA products -> fp32-equivalent ceiling
-SPLIT_PRODUCTS = {"bf16x6": 6, "f16x3": 3}
+SPLIT_PRODUCTS = {"bf16x6": 6, "f16x3": 3, "bf16": 1}
 HBM_PEAK_GBS = 8000.0
 # algorithmic FLOP per sample: forward, data-grad, weight-grad
 FLOP_FWD = 1_186_816
@@ -106,6 +106,8 @@ def kernel_roofline(k, events, math_, traffic_json):
                   f"fp32 product -> ceiling = dense bf16 peak {BF16_MFMA_PEAK_TF:.0f} / 6",
         "f16x3": "f16x3: fp32 FLOPs on v_mfma_f32_16x16x32_f16, three fp16 products per "
                  f"fp32 product -> ceiling = dense fp16 peak {BF16_MFMA_PEAK_TF:.0f} / 3",
+        "bf16": "bf16: one v_mfma_f32_16x16x32_bf16 product per product -> ceiling = dense "
+                f"bf16 peak {BF16_MFMA_PEAK_TF:.0f}",
     }.get(math_, "fp32: v_mfma_f32_32x32x2_f32 dense peak")
     return dict(bound="mfma", achieved=round(tflops, 2), peak=round(peak, 1), unit="TFLOP/s",
                 frac=round(tflops / peak, 4), flop_per_sample=flops, peak_basis=basis,
@@ -132,7 +134,12 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="budget of the CPU oracle sample (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--math", choices=("f16x3", "bf16x6", "fp32", "bf16"), default=None,
+                    help="MLP arithmetic (default: $NERF_PL_AMD_MATH or f16x3); bf16 is "
+                         "BASELINE configs[1]'s reduced-precision variant")
     a = ap.parse_args()
+    if a.math:                      # read by nerf_pl_amd.ops at import
+        os.environ["NERF_PL_AMD_MATH"] = a.math
     d = {"cfg2": (4096, 400, 64, 128), "cfg3": (4096, 504, 64, 64), "cfg4": (4096, 800, 64, 128),
          "cfg5": (512, 128, 64, 64), "eval": (32768, 400, 64, 128)}[a.config]
     a.batch = a.batch or d[0]
@@ -588,7 +595,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "bf16" if _math() == "bf16" else "fp32",
             "mlp_arithmetic": {
                 "bf16x6": "bf16x6 (fp32 operands split exactly into 3 bf16 pieces, 6 piece "
                           "products accumulated in fp32; fp32-level accuracy, parity-tested "
@@ -597,9 +604,13 @@ def main():
                          "accumulated in fp32 with power-of-two range scaling: the 3xTF32 "
                          "scheme; fp32 inputs/outputs, parity-tested against the reference "
                          "at 1e-4)",
+                "bf16": "bf16 (the reduced-precision variant of BASELINE configs[1]: matrix-core "
+                        "operands rounded once to bf16, one product, fp32 accumulation; fp32 "
+                        "activations, gradients and optimiser; judged on PSNR, not on the 1e-4 "
+                        "parity bound)",
             }.get(_math(), "fp32"),
             "data": wl["data"],
-            "config": {"workload": wl["workload"],
+            "config": {"workload": wl["workload"] + (" (bf16 MLP variant)" if _math() == "bf16" else ""),
                        "global_batch": wl["rays_per_step"] * world,
                        "samples_per_ray": wl["samples_per_ray"],
                        "parallelism": f"dp{world}" if wl["train"] else f"replicas{world}"},

@@ -109,6 +109,28 @@ int nr_mlp_bwd_h3(const void* packed_bwd, const float* head, const float* out, c
 int nr_wgrad_h3(const float* save, const float* grad_ws, int64_t n, float* workspace,
                 float* grad_flat, void* stream);
 
+/* plain bf16 arithmetic (BASELINE configs[1] "bf16/fp32": the reduced-precision
+ * MLP variant, judged on PSNR): every operand rounded once to bf16, one
+ * product per fp32 product accumulated in fp32 on v_mfma_f32_16x16x32_bf16 /
+ * 32x32x16_bf16; inputs, outputs, saved activations and gradients stay fp32.
+ * The *_b1 entry points have the contracts of their *_x3 twins; buffers:
+ * forward nr_fwd3_packed_bytes_b1() = 1,200,160 bytes (fp32 head block, then
+ * bf16 k-groups of packing.build_fwd3_map(1)), backward 1,114,112 bytes
+ * (build_bwd3_map(1)). */
+int64_t nr_fwd3_packed_bytes_b1(void);
+int nr_pack_b1(const float* flat, const int32_t* map, int64_t n, const int32_t* head_map,
+               void* out, void* stream);
+int nr_mlp_fwd_b1(const void* packed, const float* rays, const float* z, int64_t n,
+                  int samples_per_ray, const float* x, int xstride, int sigma_only, float* out,
+                  float* save, void* stream);
+int nr_mlp_sigma_points_b1(const void* packed, const float* pts, int64_t n, float* sigma_out,
+                           void* stream);
+int nr_pack_bwd_b1(const float* flat, const int32_t* map, int64_t n, void* out, void* stream);
+int nr_mlp_bwd_b1(const void* packed_bwd, const float* head, const float* out, const float* g_out,
+                  const float* save, int64_t n, float* grad_ws, void* stream);
+int nr_wgrad_b1(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                float* grad_flat, void* stream);
+
 /* Dense sigma query (extract_color_mesh.py:114-137, the marching-cubes grid):
  * sigma_out (n) = NeRF sigma head at points pts (n,3) -- the sigma-only fused
  * kernel with the positional encoding computed in-kernel (sigma does not

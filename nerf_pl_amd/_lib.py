@@ -35,6 +35,13 @@ SIGNATURES = {
     "nr_pack_bwd_h3": [_p, _p, _i64, _p, _p],
     "nr_mlp_bwd_h3": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_h3": [_p, _p, _i64, _p, _p, _p],
+    "nr_fwd3_packed_bytes_b1": [],
+    "nr_pack_b1": [_p, _p, _i64, _p, _p, _p],
+    "nr_mlp_fwd_b1": [_p, _p, _p, _i64, _i, _p, _i, _i, _p, _p, _p],
+    "nr_mlp_sigma_points_b1": [_p, _p, _i64, _p, _p],
+    "nr_pack_bwd_b1": [_p, _p, _i64, _p, _p],
+    "nr_mlp_bwd_b1": [_p, _p, _p, _p, _p, _i64, _p, _p],
+    "nr_wgrad_b1": [_p, _p, _i64, _p, _p, _p],
     "nr_mlp_bwd": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
     "nr_sm_workspace_bytes": [_i64],
@@ -61,7 +68,8 @@ SIGNATURES = {
     "nr_last_error": [],
 }
 _RESTYPES = {"nr_layout_query": _i64, "nr_adam_max_tensors": _i, "nr_fwd3_packed_bytes": _i64,
-             "nr_fwd3_packed_bytes_h3": _i64, "nr_wgrad_workspace_bytes": _i64,
+             "nr_fwd3_packed_bytes_h3": _i64, "nr_fwd3_packed_bytes_b1": _i64,
+             "nr_wgrad_workspace_bytes": _i64,
              "nr_sm_workspace_bytes": _i64, "nr_last_error": ctypes.c_char_p}
 
 _lib = None

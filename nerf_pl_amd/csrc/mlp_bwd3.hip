@@ -22,7 +22,7 @@ constexpr int kLdsBytes = kRingBytes + kMaskBytes + kHeadDma * 1024;
 struct BwdTab {
     __host__ __device__ static constexpr int64_t off(int q) { return (int64_t)q * kSlotBytes; }
 };
-static_assert(BwdTab::off(kQ) == (NR_F16 ? 2228224 : 3342336),
+static_assert(BwdTab::off(kQ) == (NR_F16 ? 2228224 : (NR_BF1 ? 1114112 : 3342336)),
               "packed size must match packing.BWD3_BYTES");
 
 // f16x3 gradient scaling.  Column (= sample) scaling commutes with the
@@ -369,6 +369,9 @@ __global__ void pack_x3_kernel(const float* __restrict__ flat, const int32_t* __
         w *= (float)(1 << kWScale);
         const float hi = (float)(_Float16)w;
         v = piece == 0 ? hi : w - hi;
+#elif NR_BF1
+        (void)piece;
+        v = (float)(__bf16)w;
 #else
         const float hi = (float)(__bf16)w;
         const float r1 = w - hi;

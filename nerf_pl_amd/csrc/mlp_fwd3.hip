@@ -39,7 +39,7 @@ struct FwdTab {
         return (int64_t)kHeadBytes + (int64_t)q * kSlotBytes;
     }
 };
-static_assert(FwdTab::off(kQAll) == (NR_F16 ? 2388000 : 3575840),
+static_assert(FwdTab::off(kQAll) == (NR_F16 ? 2388000 : (NR_BF1 ? 1200160 : 3575840)),
               "packed size must match packing.fwd3_offsets()");
 
 // w . relu(x) for both sample tiles, reduced over the 4 lane groups
@@ -461,6 +461,9 @@ __device__ __forceinline__ float weight_piece(float w, int piece) {
     w *= (float)(1 << kWScale);
     const float hi = (float)(_Float16)w;
     return piece == 0 ? hi : w - hi;
+#elif NR_BF1
+    (void)piece;
+    return (float)(__bf16)w;
 #else
     const float hi = (float)(__bf16)w;
     const float r1 = w - hi;
@@ -488,6 +491,8 @@ __global__ void pack3_kernel(const float* __restrict__ flat, const int32_t* __re
 
 #if NR_F16
 #define NR_FWD3_BYTES_NAME nr_fwd3_packed_bytes_h3
+#elif NR_BF1
+#define NR_FWD3_BYTES_NAME nr_fwd3_packed_bytes_b1
 #else
 #define NR_FWD3_BYTES_NAME nr_fwd3_packed_bytes
 #endif

@@ -35,7 +35,7 @@ enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
 // f16x3: the task pairs that read the same saved segment (wgrad_launch:
 // DZ(4), H(7), dz_dir) run fused -- one workgroup stages the shared segment
 // once and computes both outputs.  Runtime switch NR_WGRAD_FUSE=0 (host).
-constexpr bool kFuse = NR_F16;
+constexpr bool kFuse = NR_F16 || NR_BF1;
 #ifndef NR_WG_PE_WM
 #define NR_WG_PE_WM 4            // wave grid rows of the fused PE output (256 x 64)
 #endif
@@ -113,7 +113,7 @@ __device__ __forceinline__ float task_scale(const WgArgs& a, const WgTask& T) {
 #endif
 }
 
-#if !NR_F16   // the fp32-MFMA kernel lives in the bf16x6 object only
+#if NR_X3_BASE_OBJECT   // the fp32-MFMA kernel lives in the bf16x6 object only
 // Staging geometry of one 32-sample block of a segment, all compile time:
 // float4 e = tid + 512*i lands at LDS [sample j][column c].  In the
 // block-native order float4 e is (t = e>>8, q = (e>>6)&3, lane = e&63).
@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     }
 }
 
-#endif  // !NR_F16
+#endif  // NR_X3_BASE_OBJECT
 
 // ---------------------------------------------------------------------------
 // bf16x6 variant: the same task list and slabs on v_mfma_f32_32x32x16_bf16.
@@ -424,6 +424,8 @@ __device__ __forceinline__ x3::Pieces frag(const char* q, int plane) {
     f.hi = *reinterpret_cast<const x3::p8*>(q);
 #if NR_F16
     f.lo = *reinterpret_cast<const x3::p8*>(q + plane);
+#elif NR_BF1
+    (void)plane;
 #else
     f.mid = *reinterpret_cast<const x3::p8*>(q + plane);
     f.lo = *reinterpret_cast<const x3::p8*>(q + 2 * plane);
@@ -829,7 +831,7 @@ __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
 
 }  // namespace
 
-#if !NR_F16
+#if NR_X3_BASE_OBJECT
 NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
     (void)n;
     // upper bound of sum_t G_t * (M_t N_t + M_t) for the task list below
@@ -949,6 +951,8 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     stats_reduce_kernel<<<NR_STAT_SEGS, 256, 0, st>>>(SV + nr_sv_stats(nbp), (int)nbp);
     NR_LAUNCH_CHECK("nr_wgrad_stats");
     wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+#elif NR_BF1
+    wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #else
     if (x3) wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else wgrad_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
@@ -961,7 +965,7 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
 }
 }  // namespace
 
-#if !NR_F16
+#if NR_X3_BASE_OBJECT
 NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
                     float* grad_flat, void* stream) {
     return wgrad_launch(false, save, grad_ws, n, workspace, grad_flat, stream);

@@ -52,9 +52,22 @@
 #ifndef NR_F16
 #define NR_F16 0
 #endif
-// exported C-ABI names of the split-operand entry points: _x3 (bf16x6), _h3 (f16x3)
+// NR_BF1 = 1 builds the same kernels as plain "bf16": one bf16 piece per
+// operand, one product (hi*hi) per fp32 product, fp32 accumulation -- the
+// reduced-precision MLP of BASELINE configs[1] ("bf16/fp32"), judged on PSNR
+#ifndef NR_BF1
+#define NR_BF1 0
+#endif
+#if NR_F16 && NR_BF1
+#error "NR_F16 and NR_BF1 select different arithmetics"
+#endif
+// the bf16x6 object also carries the fp32-MFMA kernels and the shared entry points
+#define NR_X3_BASE_OBJECT (!NR_F16 && !NR_BF1)
+// exported C-ABI names of the split-operand entry points: _x3 (bf16x6), _h3 (f16x3), _b1 (bf16)
 #if NR_F16
 #define NR_X3_NAME(base) base##_h3
+#elif NR_BF1
+#define NR_X3_NAME(base) base##_b1
 #else
 #define NR_X3_NAME(base) base##_x3
 #endif
@@ -77,6 +90,13 @@ constexpr int kNProd = 3;                      // piece products per fp32 produc
 #define NR_H3_WSCALE 8
 #endif
 constexpr int kWScale = NR_H3_WSCALE;          // packed weights carry 2^kWScale
+#elif NR_BF1
+typedef bf16x8 p8;
+typedef bf16x2 p2;
+typedef __bf16 p1;
+constexpr int kNP = 1;
+constexpr int kNProd = 1;
+constexpr int kWScale = 0;
 #else
 typedef bf16x8 p8;
 typedef bf16x2 p2;
@@ -95,7 +115,7 @@ constexpr int kTiles = 8;                          // output tiles (16 rows) per
 // retires in issue order), so a deeper ring gives the saved-activation stores
 // more time to be acknowledged.  f16x3 groups are 16 KiB: 6 slots fit.
 #ifndef NR_X3_SLOTS
-#define NR_X3_SLOTS (NR_F16 ? 6 : 4)
+#define NR_X3_SLOTS (NR_F16 ? 6 : (NR_BF1 ? 8 : 4))
 #endif
 constexpr int kSlots = NR_X3_SLOTS;
 constexpr int kSlotBytes = kNP * kTiles * 1024;    // pieces x 8 tiles x 1 KiB
@@ -214,6 +234,8 @@ __device__ __forceinline__ void split2h(float x0, float x1, f16x2& hi, f16x2& lo
 
 #if NR_F16
 struct Pieces { p8 hi, lo; };
+#elif NR_BF1
+struct Pieces { p8 hi; };
 #else
 struct Pieces { p8 hi, mid, lo; };
 #endif
@@ -222,6 +244,8 @@ struct Pieces { p8 hi, mid, lo; };
 __device__ __forceinline__ void split_p2(float x0, float x1, p2 (&o)[kNP]) {
 #if NR_F16
     split2h(x0, x1, o[0], o[1]);
+#elif NR_BF1
+    o[0] = __builtin_convertvector((f32x2){x0, x1}, bf16x2);
 #else
     split2(x0, x1, o[0], o[1], o[2]);
 #endif
@@ -234,6 +258,7 @@ __device__ __forceinline__ void split_pair(float x0, float x1, int p, Pieces& b)
     b.hi[2 * p] = q[0][0]; b.hi[2 * p + 1] = q[0][1];
 #if NR_F16
     b.lo[2 * p] = q[1][0]; b.lo[2 * p + 1] = q[1][1];
+#elif NR_BF1
 #else
     b.mid[2 * p] = q[1][0]; b.mid[2 * p + 1] = q[1][1];
     b.lo[2 * p] = q[2][0]; b.lo[2 * p + 1] = q[2][1];
@@ -246,6 +271,8 @@ __device__ __forceinline__ void split_pair(float x0, float x1, int p, Pieces& b)
 __device__ __forceinline__ void pin(Pieces& p) {
 #if NR_F16
     asm volatile("" : "+v"(p.hi), "+v"(p.lo));
+#elif NR_BF1
+    asm volatile("" : "+v"(p.hi));
 #else
     asm volatile("" : "+v"(p.hi), "+v"(p.mid), "+v"(p.lo));
 #endif
@@ -289,13 +316,16 @@ __device__ __forceinline__ f32x4 mfma16(const p8& a, const p8& b, f32x4 c) {
 __device__ __forceinline__ void x6_pair(const Frag& w, const Pieces (&b)[2], f32x4 c0, f32x4 c1,
                                         f32x4& d0, f32x4& d1) {
     if constexpr (NR_X3_DBG == 4) {
-        asm volatile("" ::"v"(w.p[0]), "v"(w.p[kNP - 1]), "v"(b[0].hi), "v"(b[1].lo));
+        asm volatile("" ::"v"(w.p[0]), "v"(w.p[kNP - 1]), "v"(b[0].hi), "v"(b[1].hi));
         d0 = c0; d1 = c1;
         return;
     }
 #if NR_F16
     c0 = mfma16(w.p[1], b[0].hi, c0);  c1 = mfma16(w.p[1], b[1].hi, c1);
     c0 = mfma16(w.p[0], b[0].lo, c0);  c1 = mfma16(w.p[0], b[1].lo, c1);
+    d0 = mfma16(w.p[0], b[0].hi, c0);  d1 = mfma16(w.p[0], b[1].hi, c1);
+    return;
+#elif NR_BF1
     d0 = mfma16(w.p[0], b[0].hi, c0);  d1 = mfma16(w.p[0], b[1].hi, c1);
     return;
 #else
@@ -538,6 +568,8 @@ __device__ __forceinline__ f32x16 mfma_xp(const p8 (&a)[kNP], const Pieces& b, f
     acc = mfma32(a[1], b.hi, acc);
     acc = mfma32(a[0], b.lo, acc);
     acc = mfma32(a[0], b.hi, acc);
+#elif NR_BF1
+    acc = mfma32(a[0], b.hi, acc);
 #else
     acc = mfma32(a[2], b.hi, acc);
     acc = mfma32(a[0], b.lo, acc);
@@ -557,6 +589,9 @@ __device__ __forceinline__ void mfma_xp_multi(const p8 (&a)[kNP], const Pieces (
     for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[1], b[j].hi, acc[j]);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[0], b[j].lo, acc[j]);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[0], b[j].hi, acc[j]);
+#elif NR_BF1
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = mfma32(a[0], b[j].hi, acc[j]);
 #else

@@ -24,7 +24,11 @@ BLK = 32                                                # samples per block (one
 #   "bf16x6" three bf16 pieces, six products on v_mfma_f32_16x16x32_bf16
 #            (error <= 2^-25 relative per product); 2.67x
 #   "fp32"   v_mfma_f32_32x32x2_f32
-MATHS = ("f16x3", "bf16x6", "fp32")
+#   "bf16"   the reduced-precision variant of BASELINE configs[1]: operands
+#            rounded once to bf16, one product, fp32 accumulation (16x the fp32
+#            MFMA issue rate); fp32 inputs, outputs, activations and gradients.
+#            Not fp32-accurate: judged on PSNR, never the default
+MATHS = ("f16x3", "bf16x6", "fp32", "bf16")
 MATH = os.environ.get("NERF_PL_AMD_MATH", "f16x3")
 if MATH not in MATHS:
     raise ValueError(f"NERF_PL_AMD_MATH must be one of {MATHS}, got {MATH!r}")
@@ -89,8 +93,10 @@ def _maps3(device_index: int, np_: int = 3):
 FWD3_BYTES = packing.fwd3_offsets(3)[1]
 FWDH3_BYTES = packing.fwd3_offsets(2)[1]
 BWDH3_BYTES = packing.bwd3_bytes(2)
+FWDB1_BYTES = packing.fwd3_offsets(1)[1]
+BWDB1_BYTES = packing.bwd3_bytes(1)
 # C-ABI suffix of the split-operand arithmetics
-_SUFFIX = {"bf16x6": "_x3", "f16x3": "_h3"}
+_SUFFIX = {"bf16x6": "_x3", "f16x3": "_h3", "bf16": "_b1"}
 
 
 def arith_of(packed: torch.Tensor) -> str:
@@ -101,6 +107,8 @@ def arith_of(packed: torch.Tensor) -> str:
         return "bf16x6"
     if packed.numel() in (FWDH3_BYTES, BWDH3_BYTES):
         return "f16x3"
+    if packed.numel() in (FWDB1_BYTES, BWDB1_BYTES):
+        return "bf16"
     raise ValueError(f"nerf_pl_amd: unknown packed weight buffer of {packed.numel()} bytes")
 
 

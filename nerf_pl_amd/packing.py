@@ -287,8 +287,9 @@ FWD3_LAYERS = OrderedDict([          # name -> (k-steps, output halves)
     ("dir", (9, 1)),
 ])
 # pieces per operand: 3 for bf16x6 (hi, mid, lo), 2 for f16x3 (hi, lo; the
-# same layout with one piece fewer, csrc/x3.h NR_F16)
-NPIECES = {"bf16x6": 3, "f16x3": 2}
+# same layout with one piece fewer, csrc/x3.h NR_F16), 1 for plain bf16 (the
+# reduced-precision variant, csrc/x3.h NR_BF1)
+NPIECES = {"bf16x6": 3, "f16x3": 2, "bf16": 1}
 GROUP_BYTES = 3 * 8 * 1024
 HEAD_BYTES = HEAD_SIZE * 4
 

@@ -80,7 +80,7 @@ def test_pe_pairing_covers_embedding_channels():
 
 
 def test_split_operand_maps_cover_every_weight_once():
-    """bf16x6 (3 pieces) and f16x3 (2 pieces) packed maps: every weight of the
+    """bf16x6 (3 pieces), f16x3 (2 pieces) and bf16 (1 piece) packed maps: every weight of the
     forward appears once per piece; the transposed maps cover the weights the
     dgrad chain needs, once per piece; sizes match the kernels' buffers."""
     from nerf_pl_amd import packing
@@ -88,7 +88,8 @@ def test_split_operand_maps_cover_every_weight_once():
     fwd_w = np.sort(fwd_w[fwd_w >= 0])
     fwd_w = fwd_w[~np.isin(fwd_w, packing.build_fwd3_map(2)[1])]   # head entries
     bwd_w = np.sort(packing.build_bwd_map())
-    for np_, fbytes, bbytes in ((3, 3575840, 3342336), (2, 2388000, 2228224)):
+    for np_, fbytes, bbytes in ((3, 3575840, 3342336), (2, 2388000, 2228224),
+                                (1, 1200160, 1114112)):
         m, hm = packing.build_fwd3_map(np_)
         assert m.size * 2 + packing.HEAD_BYTES == packing.fwd3_offsets(np_)[1] == fbytes
         used = m[m >= 0]
