@@ -170,11 +170,12 @@ def install_timers(timer):
     from nerf_pl_amd import _lib, ops
 
     def call_tag(name, *a):
-        if name in ("nr_mlp_fwd", "nr_mlp_fwd_x3", "nr_mlp_fwd_h3"):
+        base = name[:-3] if name[-3:] in ("_x3", "_h3", "_b1") else name
+        if base == "nr_mlp_fwd":
             return ("mlp_fwd_sigma" if a[7] else "mlp_fwd"), int(a[3])
-        if name in ("nr_mlp_bwd", "nr_mlp_bwd_x3", "nr_mlp_bwd_h3"):
+        if base == "nr_mlp_bwd":
             return "mlp_bwd_dgrad", int(a[5])
-        if name in ("nr_wgrad", "nr_wgrad_x3", "nr_wgrad_h3"):
+        if base == "nr_wgrad":
             return "mlp_wgrad", int(a[2])
         if name == "nr_adam_step":
             return "adam", 0

@@ -120,10 +120,51 @@ def test_bf16_rays_path_close_to_fp32():
     assert rel < 5e-2, rel
 
 
-def test_bf16_backward_close_to_fp32(monkeypatch):
+class _LinBF16(torch.autograd.Function):
+    """nn.Linear as the bf16 kernels evaluate it (float64 otherwise): forward
+    rb(x) rb(W)^T + b (RF) or exact x W^T + b (the fp32 VALU heads);
+    data gradient rb(dy) rb(W) (RD) or exact; weight gradient always
+    rb(dy)^T rb(x) (wgrad's bf16 operands); bias gradient sum(dy) exact."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, rf, rd):
+        ctx.save_for_backward(x, w)
+        ctx.rd = rd
+        return (rb(x) @ rb(w).T if rf else x @ w.T) + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = rb(dy) @ rb(w) if ctx.rd else dy @ w
+        return dx, rb(dy).T @ rb(x), dy.sum(0), None, None
+
+
+def nerf_bf16_autograd(P, x):
+    """Oracle MLP (nerf.py:83-124) on _LinBF16 layers: forward and backward
+    with exactly the bf16 kernels' roundings."""
+    L = lambda h, name, rf=True, rd=True: _LinBF16.apply(  # noqa: E731
+        h, P[name + ".weight"], P[name + ".bias"], rf, rd)
+    xe, xd = x[:, :63], x[:, 63:]
+    h = xe
+    for i in range(8):
+        if i == 4:
+            h = torch.cat([xe, h], -1)
+        h = torch.relu(L(h, f"xyz_encoding_{i + 1}.0"))
+    sigma = L(h, "sigma", False, False)
+    feat = L(h, "xyz_encoding_final")
+    hd = torch.relu(L(torch.cat([feat, xd], -1), "dir_encoding.0"))
+    rgb = torch.sigmoid(L(hd, "rgb.0", False, False))
+    return torch.cat([rgb, sigma], -1)
+
+
+def test_bf16_backward_is_the_documented_arithmetic(monkeypatch):
     """Every parameter gradient of the bf16 MLP backward (data-gradient chain
-    + weight gradient on bf16 operands) against fp32 autograd of the oracle:
-    within a few bf16 roundings of each gradient's scale."""
+    + weight gradient) against autograd of the same arithmetic emulated in
+    float64 (_LinBF16) -- 1e-2 of each gradient's L2 norm, 3e-2 of its largest
+    entry: the two differ only in fp32 accumulation order, whose ulps
+    occasionally flip a bf16 rounding of an intermediate gradient.  The emulation itself is compared with fp32
+    autograd (bf16's own error, several % of the scale in the first layers),
+    so the test also documents what the variant gives up."""
     from nerf_pl_amd import NeRF, ops
     from nerf_pl_amd.functions import mlp_apply
     monkeypatch.setattr(ops, "MATH", "bf16")
@@ -135,31 +176,30 @@ def test_bf16_backward_close_to_fp32(monkeypatch):
                       torch.full((n_rays, 1), 2.0), torch.full((n_rays, 1), 6.0)], 1)
     z = 2 + 4 * torch.rand(n_rays, spr, generator=g)
     gout = torch.randn(n_rays * spr, 4, generator=g)
-    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
     xyz = rays[:, None, :3] + rays[:, None, 3:6] * z[..., None]
     x = torch.cat([O.embed(xyz.reshape(-1, 3), 10),
                    O.embed(rays[:, 3:6], 4).repeat_interleave(spr, 0)], 1)
-    out_ref = O.nerf_forward(pr, x)
-    (out_ref * gout).sum().backward()
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    (O.nerf_forward(pr, x) * gout).sum().backward()
+    pe = {k: v.double().clone().requires_grad_(True) for k, v in p.items()}
+    (nerf_bf16_autograd(pe, x.double()) * gout.double()).sum().backward()
     net = NeRF()
     net.load_state_dict(p)
     net = net.to(DEV)
     out = mlp_apply(net, rays=rays.to(DEV), z=z.to(DEV), spr=spr)
     assert net.packed()[0].numel() == ops.FWDB1_BYTES
     (out * gout.to(DEV)).sum().backward()
-    worst = 0.0
     for name, q in net.named_parameters():
-        ref = pr[name].grad
-        got = q.grad.cpu()
+        got = q.grad.cpu().double()
+        emu, ref = pe[name].grad, pr[name].grad.double()
         assert torch.isfinite(got).all(), name
-        rel = ((got - ref).abs().max() / (ref.abs().max() + 1e-30)).item()
-        worst = max(worst, rel)
-        assert rel < 5e-2, f"{name}: max err {rel:.3g} of the gradient's scale"
-        # and the direction of the whole gradient tensor agrees
-        cos = torch.nn.functional.cosine_similarity(got.reshape(-1).double(),
-                                                    ref.reshape(-1).double(), dim=0).item()
-        assert cos > 0.999, f"{name}: cosine {cos}"
-    assert worst > 0.0        # it is not secretly the fp32 path
+        scale = ref.abs().max().item() + 1e-30
+        err = (got - emu).abs().max().item() / scale
+        assert err < 3e-2, f"{name}: |kernel - bf16 emulation| {err:.3g} of the gradient's scale"
+        l2 = ((got - emu).norm() / (ref.norm() + 1e-30)).item()
+        assert l2 < 1e-2, f"{name}: ||kernel - bf16 emulation|| {l2:.3g} of ||gradient||"
+        cos = torch.nn.functional.cosine_similarity(got.reshape(-1), ref.reshape(-1), dim=0).item()
+        assert cos > 0.98, f"{name}: cosine with the fp32 gradient {cos}"
 
 
 def test_bf16_training_reduces_loss(monkeypatch):
