@@ -134,6 +134,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="budget of the CPU oracle sample (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: --batch rays per rank (the driver's default); strong: --batch "
+                         "rays per step in total, split over the ranks (SURVEY 8e)")
     ap.add_argument("--math", choices=("f16x3", "bf16x6", "fp32", "bf16"), default=None,
                     help="MLP arithmetic (default: $NERF_PL_AMD_MATH or f16x3); bf16 is "
                          "BASELINE configs[1]'s reduced-precision variant")
@@ -504,9 +507,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; the modulo only matters when rehearsing N ranks on
+    # fewer GPUs (NR_BENCH_DIST_BACKEND=gloo: RCCL refuses two ranks on one GPU)
+    local %= max(1, torch.cuda.device_count())
+    backend = os.environ.get("NR_BENCH_DIST_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    if args.scaling == "strong":
+        if args.batch % world:
+            raise SystemExit(f"--scaling strong: batch {args.batch} not divisible by {world} ranks")
+        args.batch //= world
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -594,7 +608,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "bf16" if _math() == "bf16" else "fp32",
             "mlp_arithmetic": {
