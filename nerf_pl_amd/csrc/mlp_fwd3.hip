@@ -127,8 +127,12 @@ __device__ __forceinline__ void dir_gather(float (&d)[8], const float* __restric
 __device__ __forceinline__ void store_pe4(const float* v, int s, int jh, int S, int g,
                                           float* __restrict__ blk, int lane) {
     const int T = 2 * s + (g >> 1), gp = 2 * (g & 1) + jh;
+#if NR_BF1
+    store_slot(f32x4{v[0], v[1], v[2], v[3]}, blk, (T * 2 + S) * 64 + 16 * gp + (lane & 15));
+#else
     *reinterpret_cast<f32x4*>(blk + ((T * 2 + S) * 64 + 16 * gp + (lane & 15)) * 4) =
         f32x4{v[0], v[1], v[2], v[3]};
+#endif
 }
 
 struct MaskWords { uint32_t w[4] = {0u, 0u, 0u, 0u}; };

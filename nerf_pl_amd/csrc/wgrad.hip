@@ -359,9 +359,15 @@ struct Stager {
             v0 = p[0]; v1 = p[1];
         } else {
             constexpr int F4 = Geo3<KIND, W>::CHUNKS * 64;
+#if NR_BF1      // bf16 segments (x3.h store_slot): 8 B per float4 slot, fp32 block stride
+            const x3::u32x2* p = reinterpret_cast<const x3::u32x2*>(base) + (size_t)blk * 2 * F4 +
+                                 Geo3<KIND, W>::f4(k, h, hb, 2 * jp);
+            v0 = x3::unpack_bf16x4(p[0]); v1 = x3::unpack_bf16x4(p[1]);
+#else
             const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * F4 +
                              Geo3<KIND, W>::f4(k, h, hb, 2 * jp);
             v0 = p[0]; v1 = p[1];
+#endif
         }
     }
     // split + store column e of this thread's chunk into an operand image
@@ -400,6 +406,15 @@ struct ThinStager {
         size_t f;   // float offset of the pair
         if constexpr (KIND == SEG_HEAD) f = 4 * ((size_t)blk * 32 + 16 * hb + j) + c;
         else f = 4 * ((size_t)blk * (W / 8) * 64 + ((c >> 4) * 2 + hb) * 64 + 16 * ((c & 15) >> 2) + j) + (c & 3);
+#if NR_BF1      // bf16 segments (the fp32 head segment aside): fp32 block stride, 2 B per element
+        if constexpr (KIND != SEG_HEAD) {
+            const size_t fb = 4 * (size_t)blk * (W / 8) * 64;    // block start, floats
+            const uint32_t u = *reinterpret_cast<const uint32_t*>(
+                reinterpret_cast<const char*>(base + fb) + 2 * (f - fb));
+            v = x3::f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+            return;
+        }
+#endif
         v = *reinterpret_cast<const x3::f32x2*>(base + f);
     }
     // split + store this thread's pair (times sc); s0/s1 += the unscaled values

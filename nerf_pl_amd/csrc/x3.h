@@ -530,8 +530,49 @@ __device__ __forceinline__ float acc_b(const f32x4 (&X)[NF][2], int s, int sb, i
 #ifndef NR_NT_STORE
 #define NR_NT_STORE 1
 #endif
+// NR_BF1 (plain bf16): a saved segment holds the values rounded to bf16 --
+// exactly what the weight gradient's bf16 MFMA operands are, so nothing is
+// lost -- element (F, S, lane, r) at bf16 index ((F * 2 + S) * 64 + lane) * 4
+// + r: one 512-B wave store per tile, half of the segment's fp32 footprint
+// (the buffers keep their fp32 sizes and offsets).
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2 pack_bf16x4(const f32x4& v) {
+    const bf16x2 a = __builtin_convertvector((f32x2){v[0], v[1]}, bf16x2);
+    const bf16x2 b = __builtin_convertvector((f32x2){v[2], v[3]}, bf16x2);
+    return u32x2{__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b)};
+}
+__device__ __forceinline__ f32x4 unpack_bf16x4(u32x2 u) {
+    return f32x4{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u),
+                 __uint_as_float(u[1] << 16), __uint_as_float(u[1] & 0xffff0000u)};
+}
+// four values (one lane's float4) to float4 slot `idx` of a saved segment
+__device__ __forceinline__ void store_slot(const f32x4& v, float* __restrict__ seg, int64_t idx) {
+#if NR_BF1
+    u32x2* p = reinterpret_cast<u32x2*>(seg) + idx;
+#if NR_X3_DBG == 9
+    asm volatile("" ::"v"(v), "v"(p));
+#elif NR_NT_STORE
+    __builtin_nontemporal_store(pack_bf16x4(v), p);
+#else
+    *p = pack_bf16x4(v);
+#endif
+#else
+    f32x4* p = reinterpret_cast<f32x4*>(seg) + idx;
+#if NR_X3_DBG == 9
+    asm volatile("" ::"v"(v), "v"(p));
+#elif NR_NT_STORE
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+#endif
+}
 __device__ __forceinline__ void store_n16(const f32x4& v, int F, int S, float* __restrict__ blk,
                                           int lane) {
+#if NR_BF1
+    store_slot(v, blk, (F * 2 + S) * 64 + lane);
+    return;
+#endif
     f32x4* p = reinterpret_cast<f32x4*>(blk + ((F * 2 + S) * 64 + lane) * 4);
 #if NR_X3_DBG == 9
     asm volatile("" ::"v"(v), "v"(p));     // timing experiment: no stores

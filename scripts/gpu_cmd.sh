@@ -1,7 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-export NR_BENCH_DIST_BACKEND=gloo
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 > gpurun_out/dist2.json 2> gpurun_out/dist2.err || { tail -20 gpurun_out/dist2.err; exit 1; }
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 --scaling strong > gpurun_out/dist2s.json 2> gpurun_out/dist2s.err || { tail -20 gpurun_out/dist2s.err; exit 2; }
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --steps 3 --warmup 1 --config cfg5 > gpurun_out/dist2c5.json 2> gpurun_out/dist2c5.err || { tail -20 gpurun_out/dist2c5.err; exit 3; }
-cat gpurun_out/dist2.json gpurun_out/dist2s.json gpurun_out/dist2c5.json | cut -c1-300
+timeout -k 10 300 python -u -m pytest tests/test_gpu_bf16.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t_bf16.log 2>&1 || { tail -30 gpurun_out/t_bf16.log; exit 1; }
+timeout -k 10 200 python bench.py --math bf16 --steps 20 --warmup 5 --cpu-baseline-seconds 0 > gpurun_out/bench_bf16.json 2> gpurun_out/bench_bf16.err || exit 2
+for s in 7 8 9; do NERF_PL_AMD_MATH=bf16 timeout -k 10 120 python scripts/psnr_compare.py --impl ours --steps 2000 --draw-seed $s --out gpurun_out/psnr_ours_bf16_s$s.json > gpurun_out/psnr_bf16_s$s.log 2>&1 || exit 3; done

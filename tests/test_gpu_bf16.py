@@ -124,19 +124,22 @@ class _LinBF16(torch.autograd.Function):
     """nn.Linear as the bf16 kernels evaluate it (float64 otherwise): forward
     rb(x) rb(W)^T + b (RF) or exact x W^T + b (the fp32 VALU heads);
     data gradient rb(dy) rb(W) (RD) or exact; weight gradient always
-    rb(dy)^T rb(x) (wgrad's bf16 operands); bias gradient sum(dy) exact."""
+    rb(dy)^T rb(x) (wgrad's bf16 operands); bias gradient sum(rb(dy)) -- the
+    variant saves every gradient segment in bf16 (csrc/x3.h store_slot) -- or,
+    for the fp32 heads (RF false), sum(dy)."""
 
     @staticmethod
     def forward(ctx, x, w, b, rf, rd):
         ctx.save_for_backward(x, w)
-        ctx.rd = rd
+        ctx.rf, ctx.rd = rf, rd
         return (rb(x) @ rb(w).T if rf else x @ w.T) + b
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dx = rb(dy) @ rb(w) if ctx.rd else dy @ w
-        return dx, rb(dy).T @ rb(x), dy.sum(0), None, None
+        db = rb(dy).sum(0) if ctx.rf else dy.sum(0)
+        return dx, rb(dy).T @ rb(x), db, None, None
 
 
 def nerf_bf16_autograd(P, x):
