@@ -213,7 +213,12 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         const int S = g;
         f32x4 v = {S ? dzr[1][0] : dzr[0][0], S ? dzr[1][1] : dzr[0][1],
                    S ? dzr[1][2] : dzr[0][2], S ? dsig[1] : dsig[0]};
+#if NR_BF1     // bf16 [block][32 samples][4] at the fp32 block stride (wgrad.hip's head DMA)
+        *reinterpret_cast<u32x2*>(reinterpret_cast<char*>(GD + nr_gd_dhead(nb) + (size_t)blk * 128) +
+                                  (16 * S + (lane & 15)) * 8) = pack_bf16x4(v);
+#else
         *reinterpret_cast<f32x4*>(GD + nr_gd_dhead(nb) + ((size_t)blk * 32 + 16 * S + (lane & 15)) * 4) = v;
+#endif
     }
     if constexpr (NR_F16) {
         float m = 0.f;

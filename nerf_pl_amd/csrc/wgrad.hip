@@ -35,7 +35,7 @@ enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
 // f16x3: the task pairs that read the same saved segment (wgrad_launch:
 // DZ(4), H(7), dz_dir) run fused -- one workgroup stages the shared segment
 // once and computes both outputs.  Runtime switch NR_WGRAD_FUSE=0 (host).
-constexpr bool kFuse = NR_F16 || NR_BF1;
+constexpr bool kFuse = NR_F16;   // (bf16: the LDS-DMA body below reads every segment once per task)
 #ifndef NR_WG_PE_WM
 #define NR_WG_PE_WM 4            // wave grid rows of the fused PE output (256 x 64)
 #endif
@@ -359,10 +359,10 @@ struct Stager {
             v0 = p[0]; v1 = p[1];
         } else {
             constexpr int F4 = Geo3<KIND, W>::CHUNKS * 64;
-#if NR_BF1      // bf16 segments (x3.h store_slot): 8 B per float4 slot, fp32 block stride
+#if NR_BF1      // bf16 segments (x3.h store_slot): 8-B slots, sample-major chunks, fp32 block stride
             const x3::u32x2* p = reinterpret_cast<const x3::u32x2*>(base) + (size_t)blk * 2 * F4 +
-                                 Geo3<KIND, W>::f4(k, h, hb, 2 * jp);
-            v0 = x3::unpack_bf16x4(p[0]); v1 = x3::unpack_bf16x4(p[1]);
+                                 x3::bf16_slot(Geo3<KIND, W>::f4(k, h, hb, 2 * jp));
+            v0 = x3::unpack_bf16x4(p[0]); v1 = x3::unpack_bf16x4(p[4]);
 #else
             const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * F4 +
                              Geo3<KIND, W>::f4(k, h, hb, 2 * jp);
@@ -406,14 +406,8 @@ struct ThinStager {
         size_t f;   // float offset of the pair
         if constexpr (KIND == SEG_HEAD) f = 4 * ((size_t)blk * 32 + 16 * hb + j) + c;
         else f = 4 * ((size_t)blk * (W / 8) * 64 + ((c >> 4) * 2 + hb) * 64 + 16 * ((c & 15) >> 2) + j) + (c & 3);
-#if NR_BF1      // bf16 segments (the fp32 head segment aside): fp32 block stride, 2 B per element
-        if constexpr (KIND != SEG_HEAD) {
-            const size_t fb = 4 * (size_t)blk * (W / 8) * 64;    // block start, floats
-            const uint32_t u = *reinterpret_cast<const uint32_t*>(
-                reinterpret_cast<const char*>(base + fb) + 2 * (f - fb));
-            v = x3::f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
-            return;
-        }
+#if NR_BF1
+        static_assert(KIND == SEG_HEAD, "bf16 runs no fused task pairs (kFuse)");
 #endif
         v = *reinterpret_cast<const x3::f32x2*>(base + f);
     }
@@ -708,8 +702,164 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
             }
 }
 
+#if NR_BF1
+// ---------------------------------------------------------------------------
+// bf16 variant: no register staging at all.  The saved segments already hold
+// the bf16 operands in sample-major 16x16 chunks (x3.h store_slot), so a
+// workgroup copies whole blocks of both operands into an LDS ring by LDS-DMA
+// (buffer_load_dwordx4 ... lds: one 1-KiB instruction per 16-feature tile,
+// kB1Depth blocks in flight) and reads its v_mfma_f32_32x32x16_bf16 fragments
+// with ds_read_b64_tr_b16 (16 lanes gather a 4-sample x 16-feature block
+// column-major: two reads = one lane's 8 consecutive samples of one
+// feature).  A tile's two 512-B chunks sit in 1152 B of LDS: the 128-B pad
+// puts the next tile's chunk in the other half of the banks, so both 16-lane
+// groups of a 32-lane half read conflict-free.  Samples past n are harmless:
+// their gradient rows are exact zeros (mlp_bwd3.hip), their inputs finite
+// copies of the last sample.  Bias sums come from the gradient fragments.
+// ---------------------------------------------------------------------------
+namespace b1 {
+constexpr int kTile = 1152;      // LDS bytes per 16-feature tile of a block
+constexpr int kDepth = 4;        // blocks in the ring
+constexpr int kLds = kDepth * 32 * kTile;   // 256 + 256 features
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// fragment rows r0 .. r0+31 (features), k-step S (samples 16S .. 16S+15) of a block image
+__device__ __forceinline__ x3::p8 frag_tr(const char* img, int r0, int S, int lane) {
+    const int g4 = lane >> 4, i = lane & 15;
+    const char* p = img + ((r0 >> 4) + (g4 & 1)) * kTile + S * 512 + 32 * (8 * (g4 >> 1) + (i >> 2)) +
+                    8 * (i & 3);
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 128));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(x3::p8, v);
+}
+
+// the head operand's fragment (HEADA): lane 4q + p of each 16-lane group
+// addresses sample 8h + q (+4) of k-step S -- all four p the same 8 B, so
+// columns 0..3 (the 4 gradient columns) are right and the rest repeat them
+__device__ __forceinline__ x3::p8 frag_head(const char* img, int S, int lane) {
+    const char* p = img + 8 * (16 * S + 8 * (lane >> 5) + ((lane & 15) >> 2));
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 32));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(x3::p8, v);
+}
+
+__device__ __forceinline__ float frag_sum(const x3::p8& f) {
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    const u32x4_t u = __builtin_bit_cast(u32x4_t, f);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += __uint_as_float(u[e] << 16) + __uint_as_float(u[e] & 0xffff0000u);
+    return s;
+}
+}  // namespace b1
+
+// HEADA: the gradient operand is the 4-column head segment [dz_rgb, dsigma],
+// bf16 [block][32 samples][4] (mlp_bwd3.hip): one 256-B dword LDS-DMA per
+// block, and every lane of a transposed read points at its sample's 4 values
+// (rows 4 .. 31 of the fragment repeat them and are never written out)
+template <int WA, int WB, int WM, int WN, bool HEADA = false>
+__device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, int b0, int b1_,
+                                              char* lds, float* __restrict__ slab) {
+    using namespace b1;
+    static_assert(!HEADA || WA == 4, "head operand");
+    constexpr int TA = HEADA ? 1 : WA / 16, TB = WB / 16, NDMA = TA + TB;
+    constexpr int ABYTES = HEADA ? 256 : TA * kTile;
+    constexpr int IMG = ABYTES + TB * kTile;
+    static_assert(kDepth * IMG <= b1::kLds, "ring");
+    constexpr int MT = (WA / WM + 31) / 32, NT = (WB / WN + 31) / 32;
+    constexpr int kWait = (kDepth - 2) * (NDMA / 8);   // this wave's DMAs issued after a block's
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool active = wave < WM * WN;
+    const int mi = wave / WN, ni = wave % WN;
+    const int m0 = 32 * MT * mi, n0 = 32 * NT * ni;
+    const __amdgpu_buffer_rsrc_t ra =
+        __builtin_amdgcn_make_buffer_rsrc((void*)T.a.base, 0, a.nb * (HEADA ? 512 : WA * 128), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb =
+        __builtin_amdgcn_make_buffer_rsrc((void*)T.b.base, 0, a.nb * WB * 128, 0x00020000);
+    // block b -> ring slot: tile i < TA of A, then the TB tiles of B, 1 KiB each
+    auto dma = [&](int b, int slot) {
+        b = min(b, b1_ - 1);      // past the end: re-read the last block (keeps vmcnt exact)
+        char* img = lds + slot * IMG;
+#pragma unroll
+        for (int i = wave; i < NDMA; i += 8) {
+            const bool isa = i < TA;
+            const int t = isa ? i : i - TA;
+            auto* dst = (__attribute__((address_space(3))) void*)(img + (isa ? i * kTile : ABYTES + t * kTile));
+            if (HEADA && isa)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 4, lane * 4, b * 512, 0, 0);
+            else
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(isa ? ra : rb, dst, 16, lane * 16,
+                                                         b * (isa ? WA : WB) * 128 + t * 1024, 0, 0);
+        }
+    };
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x16{};
+    float bsum[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) bsum[i] = 0.f;
+#pragma unroll
+    for (int d = 0; d < kDepth - 1; ++d) dma(b0 + d, d);
+#pragma unroll 1
+    for (int b = b0, it = 0; b < b1_; ++b, ++it) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory");
+        __builtin_amdgcn_s_barrier();          // every wave's DMA of block b landed; slot it-1 free
+        asm volatile("" ::: "memory");
+        dma(b + kDepth - 1, (it + kDepth - 1) % kDepth);
+        if (!active) continue;
+        const char* img = lds + (it % kDepth) * IMG;
+#pragma unroll
+        for (int S = 0; S < 2; ++S) {
+            x3::p8 bf[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bf[j] = frag_tr(img + ABYTES, n0 + 32 * j, S, lane);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const x3::p8 af = HEADA ? frag_head(img, S, lane) : frag_tr(img, m0 + 32 * i, S, lane);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[i][j] = x3::mfma32(af, bf[j], acc[i][j]);
+                if (ni == 0) bsum[i] += frag_sum(af);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's clamped DMAs
+    if (!active) return;
+    const int h = lane >> 5, col = lane & 31;
+    if (ni == 0) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const float s = bsum[i] + __shfl_xor(bsum[i], 32);
+            const int o = m0 + 32 * i + col;
+            if (h == 0 && o < WA) slab[WA * WB + o] = s;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = m0 + 32 * i + nr_acc_row(r, h);
+                const int c = n0 + 32 * j + col;
+                if (o < WA && c < WB) slab[o * WB + c] = acc[i][j][r];
+            }
+}
+#endif  // NR_BF1
+
 __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
+#if NR_BF1
+    __shared__ __attribute__((aligned(16))) char lds[b1::kLds > w3::kLds ? b1::kLds : w3::kLds];
+#else
     __shared__ __attribute__((aligned(16))) char lds[w3::kLds];
+#endif
     int t = 0;
 #pragma unroll 1
     while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
@@ -741,6 +891,22 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
         }
         return;
     }
+#if NR_BF1
+    switch (__builtin_amdgcn_readfirstlane(T.id)) {
+        case 0: case 4:
+            wgrad_b1_body<256, 64, 8, 1>(a, T, b0, b1, lds, slab); return;
+        case 10:
+            wgrad_b1_body<128, 256, 2, 4>(a, T, b0, b1, lds, slab); return;
+        case 11:
+            wgrad_b1_body<128, 32, 4, 1>(a, T, b0, b1, lds, slab); return;
+        case 12:
+            wgrad_b1_body<4, 256, 1, 8, true>(a, T, b0, b1, lds, slab); return;
+        case 13:
+            wgrad_b1_body<4, 128, 1, 4, true>(a, T, b0, b1, lds, slab); return;
+        default:
+            wgrad_b1_body<256, 256, 2, 4>(a, T, b0, b1, lds, slab); return;
+    }
+#endif
     switch (__builtin_amdgcn_readfirstlane(T.id)) {
         case 0: case 4:
             wgrad3_body<SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
@@ -919,7 +1085,9 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     int pos[kTasks];
     for (int k = 0; k < kTasks; ++k) {
         const int t = order[k];
-        const int split = cost[t] >= heavy ? 1 : 3;
+        // the 4-row head tasks' per-block time is mostly fixed cost, not
+        // bytes: always split finer, so they fill the tail of the last round
+        const int split = cost[t] >= heavy && tasks[t].a.kind != SEG_HEAD ? 1 : 3;
         int64_t g = split * ((kTargetWG * cost[t] + tot - 1) / tot);
         gt[t] = std::max<int64_t>(1, std::min<int64_t>(g, nb));
         if (!((tmask >> t) & 1)) gt[t] = 0;

@@ -532,9 +532,14 @@ __device__ __forceinline__ float acc_b(const f32x4 (&X)[NF][2], int s, int sb, i
 #endif
 // NR_BF1 (plain bf16): a saved segment holds the values rounded to bf16 --
 // exactly what the weight gradient's bf16 MFMA operands are, so nothing is
-// lost -- element (F, S, lane, r) at bf16 index ((F * 2 + S) * 64 + lane) * 4
-// + r: one 512-B wave store per tile, half of the segment's fp32 footprint
-// (the buffers keep their fp32 sizes and offsets).
+// lost.  Chunk (F, S) of a block (16 features x 16 samples, 512 B) is stored
+// sample-major: sample 16S + j, features 16F + 4g .. +3 (the lane 16g + j
+// float4 of the fp32 layout) at 8-B slot 4j + g, i.e. [sample][16 features]
+// rows of 32 B.  One wave store still covers the chunk's contiguous 512 B,
+// and wgrad.hip's LDS-DMA copies chunks as they are and reads its MFMA
+// fragments with ds_read_b64_tr_b16 (one 4-sample x 16-feature block per
+// 16 lanes).  Segments keep the fp32 block stride (buffers keep their sizes
+// and offsets), so a block uses the first half of its fp32 footprint.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u32x2 pack_bf16x4(const f32x4& v) {
     const bf16x2 a = __builtin_convertvector((f32x2){v[0], v[1]}, bf16x2);
@@ -546,9 +551,13 @@ __device__ __forceinline__ f32x4 unpack_bf16x4(u32x2 u) {
                  __uint_as_float(u[1] << 16), __uint_as_float(u[1] & 0xffff0000u)};
 }
 // four values (one lane's float4) to float4 slot `idx` of a saved segment
+// slot of the float4 idx = 64 chunk + 16 g + j of the fp32 layout in the bf16 layout
+__host__ __device__ __forceinline__ int64_t bf16_slot(int64_t idx) {
+    return (idx & ~(int64_t)63) | (4 * (idx & 15) + ((idx >> 4) & 3));
+}
 __device__ __forceinline__ void store_slot(const f32x4& v, float* __restrict__ seg, int64_t idx) {
 #if NR_BF1
-    u32x2* p = reinterpret_cast<u32x2*>(seg) + idx;
+    u32x2* p = reinterpret_cast<u32x2*>(seg) + bf16_slot(idx);
 #if NR_X3_DBG == 9
     asm volatile("" ::"v"(v), "v"(p));
 #elif NR_NT_STORE
