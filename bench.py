@@ -68,6 +68,9 @@ FLOP_TRAIN = FLOP_FWD + FLOP_DGRAD + FLOP_WGRAD   # 3,489,024
 FLOP_TRAIN_SIGMA = 2 * FLOP_FWD_SIGMA + 2 * (FLOP_FWD_SIGMA // 2 - 2 * 63 * 256)
 # weight gradient: algorithmic HBM bytes per sample (every saved segment read once)
 BYTES_WGRAD = 4 * (2528 + 2436)                     # 19,856
+# bf16 variant: every segment stored in bf16 except the 4-float head gradient
+# (itself bf16 too: 8 B/sample) -> 2 * (2528 + 2436) = 9,928
+BYTES_WGRAD_BF16 = 2 * (2528 + 2436)
 KERNEL_FLOP = {"mlp_fwd": FLOP_FWD, "mlp_fwd_sigma": FLOP_FWD_SIGMA,
                "mlp_bwd_dgrad": FLOP_DGRAD, "mlp_wgrad": FLOP_WGRAD}
 CONFIGS = ("cfg2", "cfg3", "cfg4", "cfg5", "eval")
@@ -93,11 +96,13 @@ def kernel_roofline(k, events, math_, traffic_json):
     common = dict(kernel=k, traffic=traffic, traffic_unit="GB per launch", traffic_source=tsrc,
                   samples_per_launch=nmax, avg_launch_ms=round(avg, 4))
     if k == "mlp_wgrad":
-        ach = BYTES_WGRAD * nmax / (avg * 1e-3) / 1e9
+        bps = BYTES_WGRAD_BF16 if math_ == "bf16" else BYTES_WGRAD
+        ach = bps * nmax / (avg * 1e-3) / 1e9
         return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(ach / HBM_PEAK_GBS, 4), bytes_per_sample=BYTES_WGRAD,
-                    bytes_basis="every saved activation (2528 floats/sample) and gradient "
-                                "(2436 floats/sample) segment read once",
+                    frac=round(ach / HBM_PEAK_GBS, 4), bytes_per_sample=bps,
+                    bytes_basis="every saved activation (2528 values/sample) and gradient "
+                                "(2436 values/sample) segment read once, "
+                                + ("bf16" if math_ == "bf16" else "fp32"),
                     tflops_fp32_equiv=round(tflops, 2), **common)
     np_ = SPLIT_PRODUCTS.get(math_)
     peak = BF16_MFMA_PEAK_TF / np_ if np_ else FP32_MFMA_PEAK_TF
