@@ -139,6 +139,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="budget of the CPU oracle sample (0 disables)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--light-shard", action="store_true",
+                    help="cfg5 with N>1: render the light image sharded over the ranks and "
+                         "all-gather the maps (SURVEY 8e phase 2) instead of on every rank")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="weak: --batch rays per rank (the driver's default); strong: --batch "
                          "rays per step in total, split over the ranks (SURVEY 8e)")
@@ -480,9 +483,13 @@ def wl_shadow(args, dev, rank):
         pose = sel // hw
         ppc = {"eye_pos": scene["eyes"][pose], "camera": scene["mats"][pose]}
         cam = RS.render_rays(models, emb, rays, S, False, 1.0, 0.0, I, 32768, False)
-        with torch.no_grad():
-            light = RS.render_rays(models, emb, scene["light_rays"], S, False, 1.0, 0.0, I, 32768,
-                                   False, were_gradients_computed=False)
+        if args.light_shard and dist.is_initialized() and dist.get_world_size() > 1:
+            light = RS.render_rays_sharded(models, emb, scene["light_rays"], S, False, 1.0, 0.0, I,
+                                           32768, False)
+        else:
+            with torch.no_grad():
+                light = RS.render_rays(models, emb, scene["light_rays"], S, False, 1.0, 0.0, I,
+                                       32768, False, were_gradients_computed=False)
         out = RS.efficient_sm(scene["pixels"][sel % hw], scene["light_pixels"], cam, light, ppc,
                               light_ppc, (wh, wh), I > 0, I > 0, "shadow_method_2")
         tgt = tgt_pool[sel]
@@ -496,7 +503,8 @@ def wl_shadow(args, dev, rank):
                        "re-rendered per step)",
                 workload=f"cfg5: train_efficient_sm.py step at {wh}x{wh}: sigma-only render of "
                          f"{B} camera rays/rank ({S}+{I}, noise_std=0, with gradients) + no_grad "
-                         f"render of the {hw}-ray light image ({S}+{I}) + efficient_sm "
+                         f"render of the {hw}-ray light image ({S}+{I}"
+                         f"{', sharded over the ranks + all-gather' if args.light_shard else ''}) + efficient_sm "
                          "(shadow_method_2, per-pose runs) + MSE + backward + Adam lr 5e-4",
                 data=f"synthetic ({args.poses}-pose camera orbit + one light camera, rays "
                      "generated on device, random targets, seeded default-init NeRF pair)",

@@ -301,7 +301,8 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
 // buffered; the bias sums come from the fp32 values during staging.
 // ---------------------------------------------------------------------------
 // NR_W3_DBG (timing experiments only): 1 = no MFMAs, 2 = no global loads after
-// the first stage, 3 = no LDS staging stores
+// the first stage, 3 = no LDS staging stores, 4 = input operand loaded but not
+// staged (the price of its split and LDS stores)
 #ifndef NR_W3_DBG
 #define NR_W3_DBG 0
 #endif
@@ -552,6 +553,7 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
         auto unit = [&](int u) {
             if (NR_W3_DBG == 3) return;
             if (u < 4) sa[set].store_e(ia, nval, u, bacc[u], sca);
+            else if (NR_W3_DBG == 4) asm volatile("" ::"v"(sb[set].v0), "v"(sb[set].v1));   // loads kept, no B staging
             else sb[set].store_e(ib, nval, u - 4, sdummy, 1.f);
         };
         const char* cur = lds + buf * kBufB;

@@ -1,4 +1,4 @@
-"""Data-parallel training glue (the exchange step of SURVEY.md 8e).
+"""Data-parallel training glue (the exchange steps of SURVEY.md 8e).
 
 Rays are independent, so each rank renders its own ray batch and the only
 collective is the gradient all-reduce that Lightning's DDP backend performs in
@@ -49,3 +49,40 @@ class GradAllReducer:
             dist.all_reduce(self.flat, group=self.group)
             self.flat.div_(world)
         torch._foreach_copy_(grads, self.views)
+
+
+def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None):
+    """Row-sharded evaluation of ``fn`` over the ranks of ``group``: rank r
+    applies ``fn`` to its contiguous slice of ``x`` (ceil(n / world) rows, the
+    last slice shorter) and every rank receives the whole result, each output
+    of ``fn`` (a dict of tensors with one leading row per input row) gathered
+    with one all-gather per key (``all_gather_into_tensor`` on equal, padded
+    slices).  ``rank_args(lo, hi)`` may supply extra keyword arguments for the
+    rank's slice (e.g. a replay RNG holding the slice's random draws).
+
+    Used for config 5's light image (SURVEY 8e "phase 2"): the reference
+    renders the full light image on every rank (train_efficient_sm.py:158-168);
+    sharding it divides that work by the world size at the cost of gathering
+    ~B floats per output (64 KB per map at 128^2)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n = x.shape[0]
+    per = (n + world - 1) // world
+    lo, hi = min(n, rank * per), min(n, (rank + 1) * per)
+    if hi > lo:
+        part = fn(x[lo:hi], **(rank_args(lo, hi) if rank_args else {}))
+    else:       # an empty slice still takes part in every collective (same keys)
+        part = fn(x[n - 1:n], **(rank_args(n - 1, n) if rank_args else {}))
+    out = {}
+    for k in sorted(part):
+        v = part[k]
+        if v is None:
+            out[k] = None
+            continue
+        v = v.detach()[: hi - lo]
+        buf = torch.zeros((per,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+        buf[: v.shape[0]] = v
+        full = torch.empty((world * per,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+        dist.all_gather_into_tensor(full, buf, group=group)
+        out[k] = full[:n]
+    return out

@@ -27,7 +27,7 @@ from .functions import composite_apply, mlp_apply
 from .rendering import _check_embeddings
 from .rng import STREAM_NOISE_COARSE, STREAM_NOISE_FINE, PhiloxRNG
 
-__all__ = ["render_rays", "efficient_sm"]
+__all__ = ["render_rays", "render_rays_sharded", "efficient_sm"]
 
 
 def _disp(depth, opac):
@@ -79,6 +79,30 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
         result["opacity_fine"] = opac_f
         result["disp_map_fine"] = _disp(depth_f, opac_f)
     return result
+
+
+def render_rays_sharded(models, embeddings, rays, N_samples=64, use_disp=False, perturb=0,
+                        noise_std=1, N_importance=0, chunk=1024 * 32, white_back=False,
+                        test_time=False, *, group=None, rng=None, rng_for_rows=None):
+    """The no_grad light-image render of train_efficient_sm.py:158-168 split
+    over the ranks of ``group`` (SURVEY 8e, config 5 "phase 2"): each rank
+    renders its contiguous slice of ``rays`` and all-gathers every output map
+    (``distributed.sharded_map``), instead of every rank rendering the whole
+    image as the reference does.  Per-ray results do not depend on the other
+    rays of a call, so with the same random draws the gathered maps equal the
+    replicated render bit for bit; ``rng_for_rows(lo, hi)`` supplies the draws
+    of rows lo..hi (e.g. a ReplayRNG of the sliced tensors), else each rank
+    draws from ``rng`` (default: its own Philox stream -- distribution-equivalent,
+    like the reference's per-process generators)."""
+    from .distributed import sharded_map
+
+    def fn(r, rng=rng):
+        with torch.no_grad():
+            return render_rays(models, embeddings, r.contiguous(), N_samples, use_disp, perturb,
+                               noise_std, N_importance, chunk, white_back, test_time, False,
+                               rng=rng)
+    extra = (lambda lo, hi: {"rng": rng_for_rows(lo, hi)}) if rng_for_rows else None
+    return sharded_map(fn, rays, group, extra)
 
 
 def _ppc_arrays(ppc, n):

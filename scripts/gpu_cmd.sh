@@ -1,11 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_bf16.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t_bf16.log 2>&1 || { tail -30 gpurun_out/t_bf16.log; exit 1; }
-: > gpurun_out/wg.log
-for m in bf16 f16x3; do
-  timeout -k 10 100 python dev/time_wgrad.py $m >> gpurun_out/wg.log 2>&1 || exit 1
-done
-for t in 12 13; do
-    NR_WGRAD_TASKMASK=$((1<<t)) timeout -k 10 100 python dev/time_wgrad.py bf16 >> gpurun_out/wg.log 2>&1 || exit 1
-done
-timeout -k 10 200 python bench.py --math bf16 --steps 20 --warmup 5 --cpu-baseline-seconds 0 > gpurun_out/bench_bf16.json 2> gpurun_out/bench_bf16.err || exit 2
+timeout -k 10 300 python -u -m pytest tests/test_gpu_shadow_shard.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t_shard.log 2>&1 || { tail -30 gpurun_out/t_shard.log; exit 1; }
+export NR_BENCH_DIST_BACKEND=gloo
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --steps 3 --warmup 1 --config cfg5 --light-shard > gpurun_out/dist2c5s.json 2> gpurun_out/dist2c5s.err || { tail -20 gpurun_out/dist2c5s.err; exit 3; }
+cut -c1-400 gpurun_out/dist2c5s.json

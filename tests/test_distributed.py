@@ -65,3 +65,46 @@ def test_grad_allreduce_matches_single_process():
         for a, b in zip(grads, ref):
             torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
         assert torch.all(ug == 0)
+
+
+def _shard_worker(rank, world, port, q, n):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nerf_pl_amd.distributed import sharded_map
+        x = torch.arange(n * 3, dtype=torch.float32).view(n, 3)
+        seen = []
+
+        def fn(xs, tag=None):
+            seen.append((xs.shape[0], tag))
+            return {"sum": xs.sum(1), "twice": 2 * xs, "none": None}
+        out = sharded_map(fn, x, rank_args=lambda lo, hi: {"tag": (lo, hi)})
+        q.put((rank, out["sum"], out["twice"], out["none"], seen))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_map_gathers_every_row():
+    """distributed.sharded_map (config 5's sharded light render):
+    every rank gets all n rows of every output, each row computed once by the
+    rank owning it (uneven split, and a world larger than the remainder)."""
+    for world, n in ((2, 7), (3, 2)):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q, n)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=120) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        x = torch.arange(n * 3, dtype=torch.float32).view(n, 3)
+        per = (n + world - 1) // world
+        for rank, s, t, none, seen in res:
+            torch.testing.assert_close(s, x.sum(1), rtol=0, atol=0)
+            torch.testing.assert_close(t, 2 * x, rtol=0, atol=0)
+            assert none is None
+            lo, hi = min(n, rank * per), min(n, (rank + 1) * per)
+            assert seen == [(hi - lo, (lo, hi))] if hi > lo else seen == [(1, (n - 1, n))]

@@ -1,0 +1,79 @@
+"""Config 5's light-image render sharded over ranks (SURVEY 8e "phase 2",
+rendering_shadows.render_rays_sharded): two gloo ranks on the one GPU each
+render half of the light rays with the matching rows of the reference's random
+draws, all-gather the maps, and must reproduce the replicated render
+(train_efficient_sm.py:158-168, every rank rendering every light ray) bit for
+bit -- per-ray results do not depend on the other rays of a call."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import nerf_oracle as O
+
+pytestmark = pytest.mark.gpu
+S, I, N = 32, 32, 777
+
+
+def _setup():
+    from nerf_pl_amd import Embedding, NeRF
+    from nerf_pl_amd.rays import blender_rays
+    dev = torch.device("cuda", 0)
+    models = []
+    for seed in (11, 12):
+        m = NeRF()
+        m.load_state_dict(O.make_params(seed, sigma_bias=0.5))
+        models.append(m.to(dev))
+    rays = blender_rays(32, 1, near=2.0, far=6.0)[:N].contiguous()
+    g = torch.Generator().manual_seed(5)
+    draws = [torch.rand(N, S, generator=g), torch.randn(N, S, generator=g),
+             torch.rand(N, I, generator=g), torch.rand(N, I, generator=g),
+             torch.randn(N, S + I, generator=g)]
+    return models, [Embedding(3, 10), Embedding(3, 4)], rays.to(dev), draws
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nerf_pl_amd import ReplayRNG
+        from nerf_pl_amd import rendering_shadows as RS
+        models, emb, rays, draws = _setup()
+        out = RS.render_rays_sharded(models, emb, rays, S, False, 1.0, 0.0, I, 32768, False,
+                                     rng_for_rows=lambda lo, hi: ReplayRNG([d[lo:hi] for d in draws]))
+        torch.cuda.synchronize()
+        q.put((rank, {k: v.cpu() for k, v in out.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_light_render_matches_replicated():
+    from nerf_pl_amd import ReplayRNG
+    from nerf_pl_amd import rendering_shadows as RS
+    models, emb, rays, draws = _setup()
+    with torch.no_grad():
+        ref = RS.render_rays(models, emb, rays, S, False, 1.0, 0.0, I, 32768, False,
+                             rng=ReplayRNG(draws))
+    ref = {k: v.cpu() for k, v in ref.items()}
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out in res:
+        assert sorted(out) == sorted(ref)
+        for k in ref:
+            assert torch.equal(out[k], ref[k]), (rank, k)
