@@ -1,7 +1,8 @@
 """Isolated timing of the fused MLP kernels at the cfg2 fine-pass size
 (786,432 samples), for profiling (dev tool).
 Usage: kbench.py [fwd|fwdsave|fwd3|fwd3save|bwd|bwd3|wgrad|wgrad3|fwdh3|fwdh3save|bwdh3|wgradh3
-                  |all|h3] [reps]   (x3 = bf16x6, h3 = f16x3)"""
+                  |fwdb1|fwdb1save|bwdb1|wgradb1|all|h3|b1] [reps]
+                  (x3 = bf16x6, h3 = f16x3, b1 = plain bf16)"""
 import os
 import sys
 import time
@@ -15,7 +16,8 @@ from nerf_pl_amd.functions import _wgrad_workspace
 
 FLOP = {"fwd": 1186816, "fwdsave": 1186816, "fwd3": 1186816, "fwd3save": 1186816,
         "bwd": 1115392, "bwd3": 1115392, "wgrad": 1186816, "wgrad3": 1186816,
-        "fwdh3": 1186816, "fwdh3save": 1186816, "bwdh3": 1115392, "wgradh3": 1186816}
+        "fwdh3": 1186816, "fwdh3save": 1186816, "bwdh3": 1115392, "wgradh3": 1186816,
+        "fwdb1": 1186816, "fwdb1save": 1186816, "bwdb1": 1115392, "wgradb1": 1186816}
 PEAK3 = 2516.6 / 6     # bf16 dense MFMA peak / 6 products: fp32-equivalent ceiling of bf16x6
 PEAKH3 = 2516.6 / 3    # fp16 dense MFMA peak / 3 products: ceiling of f16x3
 
@@ -29,6 +31,7 @@ def main():
     pf, pb = ops.pack_fwd_fp32(flat), ops.pack_bwd_fp32(flat)
     p3, pb3 = ops.pack_fwd3(flat), ops.pack_bwd(flat, math="bf16x6")
     ph3, pbh3 = ops.pack_fwd3(flat, math="f16x3"), ops.pack_bwd(flat, math="f16x3")
+    pb1, pbb1 = ops.pack_fwd3(flat, math="bf16"), ops.pack_bwd(flat, math="bf16")
     n_rays, spr = 4096, 192
     n = n_rays * spr
     rays = torch.randn(n_rays, 8, device=dev)
@@ -71,6 +74,14 @@ def main():
                  gout.data_ptr(), sv.data_ptr(), n, gw.data_ptr(), st)
         elif k == "wgradh3":
             call("nr_wgrad_h3", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
+        elif k in ("fwdb1", "fwdb1save"):
+            call("nr_mlp_fwd_b1", pb1.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0,
+                 0, out.data_ptr(), sv.data_ptr() if k == "fwdb1save" else None, st)
+        elif k == "bwdb1":
+            call("nr_mlp_bwd_b1", pbb1.data_ptr(), ops.head_ptr(pb1), out.data_ptr(),
+                 gout.data_ptr(), sv.data_ptr(), n, gw.data_ptr(), st)
+        elif k == "wgradb1":
+            call("nr_wgrad_b1", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
         elif k == "wgrad":
             call("nr_wgrad", sv.data_ptr(), gw.data_ptr(), n, ws.data_ptr(), gflat.data_ptr(), st)
 
@@ -78,11 +89,16 @@ def main():
         ks = ["fwd", "fwdsave", "fwd3", "fwd3save", "bwd", "bwd3", "wgrad", "wgrad3"]
     elif which == "h3":
         ks = ["fwdh3", "fwdh3save", "bwdh3", "wgradh3"]
+    elif which == "b1":
+        ks = ["fwdb1", "fwdb1save", "bwdb1", "wgradb1"]
     else:
         ks = which.split(",")
     if any("h3" in k for k in ks):   # f16x3: save buffer (and its statistics) by the h3 forward
         run("fwdh3save")
         run("bwdh3")
+    elif any("b1" in k for k in ks):   # bf16: bf16 segments written by its own kernels
+        run("fwdb1save")
+        run("bwdb1")
     else:
         run("bwd")
     for k in ks:
