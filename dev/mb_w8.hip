@@ -228,13 +228,95 @@ __device__ __forceinline__ void layer_w8(const Ring& rg, int lane, Act1& X, Act1
         *reinterpret_cast<uint2*>(msk + lane * 2) = make_uint2(mw[0], mw[1]);
 }
 
+// ============ W4, 32 KiB groups: one k-step (16 tiles) per group, 3-slot ring ======
+// the ring's slots are 2 x the 16 KiB slots above: slot index q % 3 of a 3 x 32 KiB ring
+constexpr int kBigSlots = 3, kBigBytes = 32768;
+__device__ __forceinline__ void dma_big(const Ring& r, int g, int k) {   // k = 0..7
+    const int i = r.wave + 4 * k;                 // 1 KiB fragment i of 32
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        r.rsrc, (__attribute__((address_space(3))) void*)(r.lds + (g % kBigSlots) * kBigBytes + i * 1024),
+        16, r.voff, (g % 8) * kBigBytes + i * 1024, 0, 0);
+}
+__device__ __forceinline__ void rd_big(const Ring& r, int lane, int slot, int t, Frag& f) {
+    // tile t of 16: half t >> 3 is a 16 KiB [piece 2][tile 8] block
+    const char* s = r.lds + slot * kBigBytes + (t >> 3) * 16384 + lane * 16 + (t & 7) * 1024;
+    f.hi = *reinterpret_cast<const f16x8*>(s);
+    f.lo = *reinterpret_cast<const f16x8*>(s + 8192);
+}
+__host__ __device__ constexpr int unit_big(int t) { return t >= 6 && t <= 13 ? t - 6 : -1; }
+
+template <int STORE>
+__device__ __forceinline__ void layer_w4b(const Ring& rg, int lane, Act2& X, Act2& Y, Pieces (&b)[2],
+                                          Frag& f0, float* __restrict__ sv, uint32_t* __restrict__ msk) {
+    float pend[2] = {0.f, 0.f};
+    uint32_t mw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        Pieces bn[2];
+        const int g = s;
+        Frag f[2];
+        f[0] = f0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            if (t + 1 < 16) rd_big(rg, lane, g % kBigSlots, t + 1, f[(t + 1) & 1]);
+            if (t == 15) {
+                // after DMA(g+1) (issued in group g-1): group g's 8 DMA + its stores before t 15
+                if constexpr (STORE) enter<8 + 3>(); else enter<8>();
+                rd_big(rg, lane, (g + 1) % kBigSlots, 0, f0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const Frag& w = f[t & 1];
+#pragma unroll
+            for (int S = 0; S < 2; ++S) {
+                f32x4 c = s == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : Y[t][S];
+                c = mf16(w.lo, b[S].hi, c);
+                c = mf16(w.hi, b[S].lo, c);
+                Y[t][S] = mf16(w.hi, b[S].hi, c);
+            }
+            asm volatile("" : "+a"(Y[t][0]), "+a"(Y[t][1]));
+            if (t < 8) dma_big(rg, g + kBigSlots - 1, t);
+            const int u = unit_big(t);
+            if (u >= 0) {
+                const int S = u >> 2, p = u & 3;
+                const int F = s < 7 ? 2 * (s + 1) + (p >> 1) : (p >> 1);
+                const f32x4& src = s < 7 ? X[F][S] : Y[F][S];
+                f16x2 h, l;
+                float u0, u1;
+                split_pair(src[2 * (p & 1)], src[2 * (p & 1) + 1], h, l, u0, u1);
+                put(bn[S], p, h, l);
+                pin(bn[S]);
+                if constexpr (STORE) {
+                    if ((p & 1) == 0) { pend[0] = u0; pend[1] = u1; }
+                    else {
+                        const f32x4 v = {pend[0], pend[1], u0, u1};
+                        store4(v, sv + ((F * 2 + S) * 64 + lane) * 4);
+                        mask4(v, 8 * (F & 3) + 4 * S, mw[F >> 2]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, MB_SGB, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        b[0] = bn[0];
+        b[1] = bn[1];
+    }
+    if constexpr (STORE)
+        *reinterpret_cast<uint4*>(msk + lane * 4) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+}
+
 // samples per workgroup: 128 in both layouts
-template <int NW, int STORE>
-__global__ void __launch_bounds__(64 * NW, 1) mb_kernel(const char* __restrict__ w, int pairs,
+template <int NW_, int STORE>
+__global__ void __launch_bounds__(64 * (NW_ == 5 ? 4 : NW_), 1) mb_kernel(const char* __restrict__ w, int pairs,
                                                         float* __restrict__ save, float* __restrict__ out,
                                                         uint64_t* __restrict__ stamps) {
+    constexpr int NW = NW_ == 5 ? 4 : NW_;
+    constexpr bool BIG = NW_ == 5;
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    __shared__ __attribute__((aligned(16))) char lds[kSlots * kSlotBytes];
+    __shared__ __attribute__((aligned(16))) char lds[BIG ? kBigSlots * kBigBytes : kSlots * kSlotBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wv = blockIdx.x * NW + wave;          // wave index in the grid
@@ -243,10 +325,17 @@ __global__ void __launch_bounds__(64 * NW, 1) mb_kernel(const char* __restrict__
     rg.lds = lds;
     rg.wave = wave;
     rg.voff = lane * 16;
+    if constexpr (BIG) {
 #pragma unroll
-    for (int g = 0; g < kSlots - 1; ++g)
+        for (int g = 0; g < kBigSlots - 1; ++g)
 #pragma unroll
-        for (int k = 0; k < 16 / NW; ++k) dma<NW>(rg, g, k);
+            for (int k = 0; k < 8; ++k) dma_big(rg, g, k);
+    } else {
+#pragma unroll
+        for (int g = 0; g < kSlots - 1; ++g)
+#pragma unroll
+            for (int k = 0; k < 16 / NW; ++k) dma<NW>(rg, g, k);
+    }
     const float seed = (float)(wv * 64 + lane) * 1e-4f;
     Frag f0;
     float acc_sum = 0.f;
@@ -272,13 +361,19 @@ __global__ void __launch_bounds__(64 * NW, 1) mb_kernel(const char* __restrict__
             put(b[S], p, h, l);
         }
         enter<0>();
-        rd(rg, lane, 0, 0, f0);
+        if constexpr (BIG) rd_big(rg, lane, 0, 0, f0);
+        else rd(rg, lane, 0, 0, f0);
         for (int it = 0; it < pairs; ++it) {
             float* sv = save + ((size_t)(wv * pairs + it) * 2) * kLayerFloats;
             uint32_t* mk = reinterpret_cast<uint32_t*>(save) + nwaves * pairs * 2 * kLayerFloats +
                            ((size_t)(wv * pairs + it) * 2) * kMaskWords;
-            layer_w4<STORE>(rg, lane, X, Y, b, f0, sv, mk);
-            layer_w4<STORE>(rg, lane, Y, X, b, f0, sv + kLayerFloats, mk + kMaskWords);
+            if constexpr (BIG) {
+                layer_w4b<STORE>(rg, lane, X, Y, b, f0, sv, mk);
+                layer_w4b<STORE>(rg, lane, Y, X, b, f0, sv + kLayerFloats, mk + kMaskWords);
+            } else {
+                layer_w4<STORE>(rg, lane, X, Y, b, f0, sv, mk);
+                layer_w4<STORE>(rg, lane, Y, X, b, f0, sv + kLayerFloats, mk + kMaskWords);
+            }
         }
 #pragma unroll
         for (int F = 0; F < 16; ++F) acc_sum += X[F][0][0] + X[F][1][3];
@@ -318,15 +413,16 @@ __global__ void __launch_bounds__(64 * NW, 1) mb_kernel(const char* __restrict__
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
-template <int NW, int STORE>
+template <int NW_, int STORE>
 void bench(const char* w, int blocks, int pairs, float* save, float* out, uint64_t* stamps, int reps) {
+    constexpr int NW = NW_ == 5 ? 4 : NW_;
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int i = 0; i < 3; ++i) mb_kernel<NW, STORE><<<blocks, 64 * NW>>>(w, pairs, save, out, stamps);
+    for (int i = 0; i < 3; ++i) mb_kernel<NW_, STORE><<<blocks, 64 * NW>>>(w, pairs, save, out, stamps);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(a));
-    for (int i = 0; i < reps; ++i) mb_kernel<NW, STORE><<<blocks, 64 * NW>>>(w, pairs, save, out, stamps);
+    for (int i = 0; i < reps; ++i) mb_kernel<NW_, STORE><<<blocks, 64 * NW>>>(w, pairs, save, out, stamps);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -338,8 +434,8 @@ void bench(const char* w, int blocks, int pairs, float* save, float* out, uint64
     double cyc = 0, rt = 0;
     for (int i = 0; i < blocks; ++i) { cyc += hs[2 * i]; rt += hs[2 * i + 1]; }
     free(hs);
-    printf("waves %d store %d slots %d sgb %d: %.3f ms  %.1f TF fp32-equiv (%.1f%% of 839)  clock %.2f GHz  WG %.0f cyc\n",
-           NW, STORE, kSlots, MB_SGB, ms, flop / ms / 1e9, flop / ms / 1e9 / 8.389, cyc / rt * 0.1, cyc / blocks);
+    printf("waves %d%s store %d slots %d sgb %d: %.3f ms  %.1f TF fp32-equiv (%.1f%% of 839)  clock %.2f GHz  WG %.0f cyc\n",
+           NW, NW_ == 5 ? " (32 KiB groups)" : "", STORE, NW_ == 5 ? kBigSlots : kSlots, MB_SGB, ms, flop / ms / 1e9, flop / ms / 1e9 / 8.389, cyc / rt * 0.1, cyc / blocks);
     CK(hipEventDestroy(a));
     CK(hipEventDestroy(b));
 }
@@ -349,7 +445,7 @@ int main(int argc, char** argv) {
     char* w;
     float *save, *out;
     uint64_t* stamps;
-    CK(hipMalloc(&w, kGroups * kSlotBytes));
+    CK(hipMalloc(&w, kGroups * kSlotBytes));   // 16 x 16 KiB = 8 x 32 KiB
     uint16_t* hw = (uint16_t*)malloc(kGroups * kSlotBytes);
     srand(1);
     for (int i = 0; i < kGroups * kSlotBytes / 2; ++i) {
@@ -363,8 +459,10 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&stamps, (size_t)blocks * 16));
     for (int r = 0; r < 2; ++r) {
         bench<4, 0>(w, blocks, pairs, save, out, stamps, reps);
+        bench<5, 0>(w, blocks, pairs, save, out, stamps, reps);
         bench<8, 0>(w, blocks, pairs, save, out, stamps, reps);
         bench<4, 1>(w, blocks, pairs, save, out, stamps, reps);
+        bench<5, 1>(w, blocks, pairs, save, out, stamps, reps);
         bench<8, 1>(w, blocks, pairs, save, out, stamps, reps);
     }
     return 0;

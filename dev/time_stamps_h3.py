@@ -1,0 +1,46 @@
+"""f16x3 forward clock stamps (dev only; dev/libh3_dbg8.so = mlp_fwd3.hip with
+-DNR_F16=1 -DNR_X3_DBG=8): per wave the in-kernel clock, total cycles and the
+prologue's cycles (inputs, positional encoding, first weight group)."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from nerf_pl_amd import ops, packing  # noqa: E402
+from nerf_pl_amd._lib import stream_of  # noqa: E402
+
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+flat = (torch.rand(packing.N_PARAMS, device=dev) - 0.5) * 0.15
+ph = ops.pack_fwd3(flat, math="f16x3")
+n_rays, spr = 4096, 192
+n = n_rays * spr
+rays = torch.randn(n_rays, 8, device=dev)
+rays[:, 3:6] = torch.nn.functional.normalize(rays[:, 3:6], dim=-1)
+rays[:, 6], rays[:, 7] = 2.0, 6.0
+z = (torch.rand(n, device=dev) * 4 + 2).contiguous()
+out = torch.empty(n, 4, device=dev)
+L = ctypes.CDLL(os.path.abspath("dev/libh3_dbg8.so"))
+f = L.nr_mlp_fwd_h3
+P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+f.argtypes = [P, P, P, I64, I, P, I, I, P, P, P]
+nb = (n + 31) // 32
+stp = torch.zeros(nb * 4, dtype=torch.int64, device=dev)
+st = stream_of(dev)
+for _ in range(30):
+    f(ph.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0, out.data_ptr(), stp.data_ptr(), st)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(10):
+    f(ph.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0, out.data_ptr(), stp.data_ptr(), st)
+e1.record()
+torch.cuda.synchronize()
+w = stp.view(nb, 4).cpu().double()
+dt_real = (w[:, 1] - w[:, 0]).clamp(min=1)
+clock = w[:, 2] / dt_real * 100
+print(f"fwd (no save) {e0.elapsed_time(e1) / 10:.3f} ms; clock median {clock.median().item():.0f} MHz; "
+      f"wave cycles median {w[:, 2].median().item():.0f}; prologue cycles median {w[:, 3].median().item():.0f} "
+      f"(p90 {w[:, 3].quantile(0.9).item():.0f}); waves x rounds: {nb} waves / 1024 SIMDs", flush=True)

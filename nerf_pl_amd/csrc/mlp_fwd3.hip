@@ -329,6 +329,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 
     Frag f0;           // tile-0 fragments of the next k-group
     enter<0, QEND>(smem, lane, f0);
+#if NR_X3_DBG == 8
+    const uint64_t t_pro = __builtin_amdgcn_s_memtime() - t0;   // prologue: inputs, PE, first group
+#endif
 
     Act A, B;
     Pieces b[2];       // pieces of the next k-step
@@ -436,7 +439,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             st[0] = r0;
             st[1] = __builtin_amdgcn_s_memrealtime();
             st[2] = __builtin_amdgcn_s_memtime() - t0;
-            st[3] = 0;
+            st[3] = t_pro;
         }
 #endif
         if constexpr (SAVE) {

@@ -1,8 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-for tag in h3 b1; do
-  for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 240 rocprofv3 --kernel-trace --pmc $c -d gpurun_out/pmc_r02_$tag/$c -o run --output-format csv -- python scripts/kbench.py $tag 3 > gpurun_out/pmc_r02_${tag}_$c.log 2>&1 || { tail -5 gpurun_out/pmc_r02_${tag}_$c.log; exit 1; }
-  done
-done
-python scripts/kbench.py h3 10 > gpurun_out/kbench_h3.log 2>&1 && python scripts/kbench.py b1 10 > gpurun_out/kbench_b1.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t_all.log 2>&1 || { tail -30 gpurun_out/t_all.log; exit 1; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 2; }
+timeout -k 10 300 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 3; }
+tail -2 gpurun_out/t_all.log; tail -2 gpurun_out/smoke.log; cut -c1-300 gpurun_out/bench_default.json
