@@ -219,8 +219,11 @@ def install_timers(timer):
 # CPU baselines: the oracle (reference algorithm, PyTorch CPU) on a bounded
 # sample of the same workload, on this host's cores
 # ---------------------------------------------------------------------------
+_CPU_THREADS = None      # set for the single-thread row
+
+
 def _cpu_threads():
-    t = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    t = _CPU_THREADS or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(t)
     return t
 
@@ -608,8 +611,17 @@ def main():
         ks[dom]["share_of_step"] = ks[dom]["total_ms"] / (ms * args.steps)
 
     cpu = None
+    cpu1 = None
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
         cpu = wl["cpu"](args.cpu_baseline_seconds)
+        # "... and a 1-thread row too" (a third of the budget)
+        global _CPU_THREADS
+        _CPU_THREADS = 1
+        try:
+            cpu1 = wl["cpu"](args.cpu_baseline_seconds / 3)
+        finally:
+            _CPU_THREADS = None
+            _cpu_threads()
 
     if rank == 0:
         line = {
@@ -646,6 +658,7 @@ def main():
             "roofline": roof,
             "rooflines": roofs,
             "cpu_baseline": cpu,
+            "cpu_baseline_1thread": cpu1,
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv
                             for kk, vv in v.items()} for k, v in ks.items()},
             "final_loss": round(loss.item(), 5) if loss is not None else None,

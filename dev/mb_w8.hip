@@ -92,6 +92,9 @@ __device__ __forceinline__ f32x4 mf16(const f16x8& a, const f16x8& b, f32x4 c) {
 #ifndef MB_SGB
 #define MB_SGB 1
 #endif
+#ifndef MB_DMA
+#define MB_DMA 1
+#endif
 
 // ============ W4: 2 sample tiles per wave (mlp_fwd3 today) ===================
 typedef f32x4 Act2[16][2];
@@ -114,7 +117,8 @@ __device__ __forceinline__ void layer_w4(const Ring& rg, int lane, Act2& X, Act2
             for (int t = 0; t < 8; ++t) {
                 if (t + 1 < 8) rd(rg, lane, g % kSlots, t + 1, f[(t + 1) & 1]);
                 if (t == 7) {
-                    if constexpr (STORE) enter<14>(); else enter<8>();
+                    if constexpr (MB_DMA == 0) { if constexpr (STORE) enter<6>(); else enter<0>(); }
+                    else if constexpr (STORE) enter<14>(); else enter<8>();
                     rd(rg, lane, (g + 1) % kSlots, 0, f0);
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -127,7 +131,12 @@ __device__ __forceinline__ void layer_w4(const Ring& rg, int lane, Act2& X, Act2
                     Y[8 * hf + t][S] = mf16(w.hi, b[S].hi, c);
                 }
                 asm volatile("" : "+a"(Y[8 * hf + t][0]), "+a"(Y[8 * hf + t][1]));
+#if MB_DMA == 0        // no weight DMA after the prologue (the ring keeps stale weights): its price
+#elif MB_DMA == 2      // spread over the odd tiles
+                if (t & 1) dma<4>(rg, g + kSlots - 1, t >> 1);
+#else
                 if (t < 4) dma<4>(rg, g + kSlots - 1, t);
+#endif
                 const int u = unit_at2(t, hf);
                 if (u >= 0) {
                     const int S = u >> 2, p = u & 3;

@@ -27,7 +27,7 @@ f = L.nr_mlp_fwd_h3
 P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
 f.argtypes = [P, P, P, I64, I, P, I, I, P, P, P]
 nb = (n + 31) // 32
-stp = torch.zeros(nb * 4, dtype=torch.int64, device=dev)
+stp = torch.zeros(nb * 16, dtype=torch.int64, device=dev)
 st = stream_of(dev)
 for _ in range(30):
     f(ph.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0, out.data_ptr(), stp.data_ptr(), st)
@@ -38,9 +38,20 @@ for _ in range(10):
     f(ph.data_ptr(), rays.data_ptr(), z.data_ptr(), n, spr, None, 0, 0, out.data_ptr(), stp.data_ptr(), st)
 e1.record()
 torch.cuda.synchronize()
-w = stp.view(nb, 4).cpu().double()
+w = stp.view(nb, 16).cpu().double()
 dt_real = (w[:, 1] - w[:, 0]).clamp(min=1)
 clock = w[:, 2] / dt_real * 100
+names = ["inputs+PE", "first group", "L1 (2 ks)", "L2", "L3", "L4", "L5 PE (2 ks)", "L5 h4", "L6", "L7",
+         "L8", "final", "dir (9 groups)"]
+groups = [0, 0, 4, 16, 16, 16, 4, 16, 16, 16, 16, 16, 9]
+st_ = w[:, 3:16]
+prev = torch.zeros(nb, dtype=torch.float64)
 print(f"fwd (no save) {e0.elapsed_time(e1) / 10:.3f} ms; clock median {clock.median().item():.0f} MHz; "
-      f"wave cycles median {w[:, 2].median().item():.0f}; prologue cycles median {w[:, 3].median().item():.0f} "
-      f"(p90 {w[:, 3].quantile(0.9).item():.0f}); waves x rounds: {nb} waves / 1024 SIMDs", flush=True)
+      f"wave cycles median {w[:, 2].median().item():.0f}", flush=True)
+for i, (nm, gq) in enumerate(zip(names, groups)):
+    d = (st_[:, i] - prev).median().item()
+    prev = st_[:, i]
+    ideal = gq * 768
+    print(f"  {nm:16s} {d:8.0f} cycles" + (f"  ({gq} groups: {d / gq:6.0f}/group, MFMA-only 768)" if gq else ""),
+          flush=True)
+print(f"  {'heads + end':16s} {(w[:, 2] - st_[:, 12]).median().item():8.0f} cycles", flush=True)

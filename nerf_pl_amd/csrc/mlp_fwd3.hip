@@ -244,6 +244,15 @@ struct PeU {
     }
 };
 
+// NR_X3_DBG 8 (dev timing build): per-layer clock stamps, 16 uint64 per wave
+// in the save pointer: [0] start realtime, [1] end realtime, [2] cycles,
+// [3 + i] cycles at stamp i (0 inputs+PE, 1 first hand-over, 2.. segments)
+#if NR_X3_DBG == 8
+#define NR_STAMP(i) (stamps[i] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0))
+#else
+#define NR_STAMP(i) ((void)0)
+#endif
+
 template <int MODE, bool SIGMA_ONLY, bool SAVE>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     constexpr bool EMB = MODE == FWD_EMB;
@@ -264,6 +273,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     const char* P = a.packed;
 #if NR_X3_DBG == 8
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t stamps[13] = {};
 #endif
 
     // sample inputs first: they are waited for while the weight DMA below
@@ -326,12 +336,14 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             pe_lds[(9 + 2 * S) * 64] = f32x4{dg[S][4], dg[S][5], dg[S][6], dg[S][7]};
         }
     }
+#if NR_X3_DBG == 8
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    NR_STAMP(0);       // inputs + positional encoding
 
     Frag f0;           // tile-0 fragments of the next k-group
     enter<0, QEND>(smem, lane, f0);
-#if NR_X3_DBG == 8
-    const uint64_t t_pro = __builtin_amdgcn_s_memtime() - t0;   // prologue: inputs, PE, first group
-#endif
+    NR_STAMP(1);       // prologue: + first weight group
 
     Act A, B;
     Pieces b[2];       // pieces of the next k-step
@@ -354,10 +366,13 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         auto bi = bias(NR_H_BIAS(1));
         segment<FwdTab, kL1, 2, 2, QEND, true>(dma, lane, A, peu, u1, bi, side, b, f0);
     }
+    NR_STAMP(2);
     U u2{B, hseg(1), mseg(1), nullptr, lane, g};
     { auto bi = bias(NR_H_BIAS(2)); segment<FwdTab, kL2, 8, 2, QEND, true>(dma, lane, B, u1, u2, bi, none, b, f0); }
+    NR_STAMP(3);
     U u3{A, hseg(2), mseg(2), nullptr, lane, g};
     { auto bi = bias(NR_H_BIAS(3)); segment<FwdTab, kL3, 8, 2, QEND, true>(dma, lane, A, u2, u3, bi, none, b, f0); }
+    NR_STAMP(4);
     float pe5[2][16];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -367,15 +382,20 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     }
     PeU<16> pe5u{pe5};
     { auto bi = bias(NR_H_BIAS(4)); segment<FwdTab, kL4, 8, 2, QEND, true>(dma, lane, B, u3, pe5u, bi, none, b, f0); }
+    NR_STAMP(5);
     // layer 5: cat[PE, h4] -> 256 (nerf.py:108-109)
     U u4{B, hseg(3), mseg(3), nullptr, lane, g};
     { auto bi = bias(NR_H_BIAS(5)); segment<FwdTab, kL5, 2, 2, QEND, true>(dma, lane, A, pe5u, u4, bi, none, b, f0); }
+    NR_STAMP(6);
     U u5{A, hseg(4), mseg(4), nullptr, lane, g};
     segment<FwdTab, kL5 + 4, 8, 2, QEND, false>(dma, lane, A, u4, u5, zero, none, b, f0);
+    NR_STAMP(7);
     U u6{B, hseg(5), mseg(5), nullptr, lane, g};
     { auto bi = bias(NR_H_BIAS(6)); segment<FwdTab, kL6, 8, 2, QEND, true>(dma, lane, B, u5, u6, bi, none, b, f0); }
+    NR_STAMP(8);
     U u7{A, hseg(6), mseg(6), nullptr, lane, g};
     { auto bi = bias(NR_H_BIAS(7)); segment<FwdTab, kL7, 8, 2, QEND, true>(dma, lane, A, u6, u7, bi, none, b, f0); }
+    NR_STAMP(9);
 
     // lane group g < 2 writes sample tile S = g
     const int Sw = g & 1;
@@ -391,6 +411,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         // h8 feeds xyz_encoding_final and, while it is split, the sigma head
         AccU<true, SAVE, SAVE, true> u8{B, hseg(7), mseg(7), H + NR_H_WSIG, lane, g};
         { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, u8, bi, none, b, f0); }
+        NR_STAMP(10);
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
         float dpe[2][8];
 #pragma unroll
@@ -406,6 +427,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         AccU<false, SAVE, false, false> uf{A, SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256),
                                            nullptr, nullptr, lane, g};
         { auto bi = bias(NR_H_BFINAL); segment<FwdTab, kFinal, 8, 2, QEND, true>(dma, lane, A, u8, uf, bi, none, b, f0); }
+        NR_STAMP(11);
         float sigma[2];
 #pragma unroll
         for (int S = 0; S < 2; ++S) {
@@ -420,6 +442,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             DirPeSide<SAVE> side{dpe, SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32), g, lane};
             segment<FwdTab, kDir + 8, 1, 1, QEND, false>(dma, lane, C, dpeu, nonext, zero, side, b, f0);
         }
+        NR_STAMP(12);
         float zc[3][2];
 #pragma unroll
         for (int c = 0; c < 3; ++c) head_dot<true>(C, H + NR_H_WRGB + 128 * c, g, zc[c]);
@@ -435,11 +458,11 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         }
 #if NR_X3_DBG == 8
         if (lane == 0) {
-            uint64_t* st = reinterpret_cast<uint64_t*>(a.save) + (size_t)blk * 4;
+            uint64_t* st = reinterpret_cast<uint64_t*>(a.save) + (size_t)blk * 16;
             st[0] = r0;
             st[1] = __builtin_amdgcn_s_memrealtime();
             st[2] = __builtin_amdgcn_s_memtime() - t0;
-            st[3] = t_pro;
+            for (int i = 0; i < 13; ++i) st[3 + i] = stamps[i];
         }
 #endif
         if constexpr (SAVE) {

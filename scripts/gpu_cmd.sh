@@ -1,6 +1,2 @@
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t_all.log 2>&1 || { tail -30 gpurun_out/t_all.log; exit 1; }
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 2; }
-timeout -k 10 300 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 3; }
-tail -2 gpurun_out/t_all.log; tail -2 gpurun_out/smoke.log; cut -c1-300 gpurun_out/bench_default.json
+for v in mb_w8 mb_w8_dma0 mb_w8_dma2; do echo "== $v"; timeout -k 5 120 ./dev/$v 20; done > gpurun_out/w8dma.log 2>&1
