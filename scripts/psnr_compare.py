@@ -111,6 +111,13 @@ def import_reference():
     return ref_nerf, ref_rendering
 
 
+def initial_params(seed: int, perturb_ulp: bool):
+    p = make_params(seed)
+    if perturb_ulp:
+        p = {k: torch.nextafter(v, torch.full_like(v, math.inf)) for k, v in p.items()}
+    return p
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--impl", choices=["ours", "reference"], required=True)
@@ -120,6 +127,14 @@ def main():
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--draw-seed", type=int, default=7,
                     help="seed of the render draws (run-to-run spread: vary it)")
+    ap.add_argument("--perturb-ulp", action="store_true",
+                    help="move every initial parameter up by one fp32 ulp (control run: the "
+                         "PSNR spread that an ulp-level difference alone produces)")
+    ap.add_argument("--save-weights", default=None,
+                    help="write the trained parameters (safetensors) for --eval-weights")
+    ap.add_argument("--eval-weights", default=None,
+                    help="no training: render the held-out views with these trained "
+                         "parameters and report the PSNR (same-weights renderer parity)")
     ap.add_argument("--out", default=None, help="JSON path (default profiles/r01/psnr_<impl>.json)")
     args = ap.parse_args()
     torch.set_num_threads(args.threads or min(16, os.cpu_count() or 1))
@@ -132,7 +147,7 @@ def main():
         models = []
         for s in (101, 102):
             m = NeRF()
-            m.load_state_dict(make_params(s))
+            m.load_state_dict(initial_params(s, args.perturb_ulp))
             models.append(m.to(dev))
         emb = [Embedding(3, 10), Embedding(3, 4)]
         draws = CPUDraws()
@@ -146,7 +161,7 @@ def main():
         models = []
         for s in (101, 102):
             m = ref_nerf.NeRF()
-            m.load_state_dict(make_params(s))
+            m.load_state_dict(initial_params(s, args.perturb_ulp))
             models.append(m)
         emb = [ref_nerf.Embedding(3, 10), ref_nerf.Embedding(3, 4)]
 
@@ -168,6 +183,27 @@ def main():
         print(json.dumps(log[-1]), flush=True)
 
     t0 = time.time()
+    if args.eval_weights:
+        from safetensors.torch import load_file
+        sd = load_file(args.eval_weights)
+        for tag, m in zip(("coarse", "fine"), models):
+            m.load_state_dict({k[len(tag) + 1:]: v.to(dev) for k, v in sd.items()
+                               if k.startswith(tag + ".")})
+        with torch.no_grad():
+            pred = torch.cat([render(test[i:i + 4096])["rgb_fine"].cpu()
+                              for i in range(0, test.shape[0], 4096)])
+        p = float(-10.0 * torch.log10(torch.mean((pred - test_rgb) ** 2)))
+        path = args.out or os.path.join(REPO, "profiles", "r02", f"psnr_eval_{args.impl}.json")
+        np.save(path[:-5] + "_pred.npy", pred.numpy())
+        out = {"impl": args.impl, "eval_weights": os.path.basename(args.eval_weights),
+               "draw_seed": args.draw_seed, "psnr": p}
+        if args.impl == "ours":
+            from nerf_pl_amd import ops
+            out["mlp_arithmetic"] = ops.MATH
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps(out))
+        return
     for step in range(1, args.steps + 1):
         idx = torch.randint(0, train.shape[0], (args.batch,), generator=gen)
         rays, tgt = train[idx].to(dev), train_rgb[idx].to(dev)
@@ -185,7 +221,12 @@ def main():
             state = torch.get_rng_state()
             evaluate(step)
             torch.set_rng_state(state)
-    out = {"impl": args.impl, "steps": args.steps, "batch": args.batch, "samples": [S, I],
+    if args.save_weights:
+        from safetensors.torch import save_file
+        save_file({f"{tag}.{k}": v.detach().cpu().contiguous()
+                   for tag, m in zip(("coarse", "fine"), models)
+                   for k, v in m.state_dict().items()}, args.save_weights)
+    out = {"impl": args.impl, "steps": args.steps, "perturb_ulp": args.perturb_ulp, "batch": args.batch, "samples": [S, I],
            "img": IMG, "train_views": 24, "test_views": 2, "draw_seed": args.draw_seed, "psnr": log, "loss": losses,
            "final_psnr": log[-1]["psnr"] if log else None,
            "threads": torch.get_num_threads() if args.impl == "reference" else None}
