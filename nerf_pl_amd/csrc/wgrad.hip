@@ -780,13 +780,18 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
     const bool active = wave < WM * WN;
     const int mi = wave / WN, ni = wave % WN;
     const int m0 = 32 * MT * mi, n0 = 32 * NT * ni;
-    const __amdgpu_buffer_rsrc_t ra =
-        __builtin_amdgcn_make_buffer_rsrc((void*)T.a.base, 0, a.nb * (HEADA ? 512 : WA * 128), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rb =
-        __builtin_amdgcn_make_buffer_rsrc((void*)T.b.base, 0, a.nb * WB * 128, 0x00020000);
+    // the resources start at this workgroup's first block: buffer offsets and
+    // sizes are 32-bit, and a whole segment passes 2^31 bytes at 2^16 blocks
+    // (2.1M samples per call) while one workgroup's slice stays far below
+    constexpr int64_t ABLK = HEADA ? 512 : WA * 128, BBLK = WB * 128;
+    const int nblk = b1_ - b0;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(reinterpret_cast<const char*>(T.a.base) + (int64_t)b0 * ABLK), 0, (int)(nblk * ABLK), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(reinterpret_cast<const char*>(T.b.base) + (int64_t)b0 * BBLK), 0, (int)(nblk * BBLK), 0x00020000);
     // block b -> ring slot: tile i < TA of A, then the TB tiles of B, 1 KiB each
     auto dma = [&](int b, int slot) {
-        b = min(b, b1_ - 1);      // past the end: re-read the last block (keeps vmcnt exact)
+        b = min(b, b1_ - 1) - b0; // past the end: re-read the last block (keeps vmcnt exact)
         char* img = lds + slot * IMG;
 #pragma unroll
         for (int i = wave; i < NDMA; i += 8) {

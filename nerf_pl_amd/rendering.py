@@ -62,6 +62,11 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
     rays = ops._dev(rays, "rays", 8)
     dev = rays.device
     n_rays = rays.shape[0]
+    if n_rays == 0:
+        # the reference fails here too: its chunk loop yields no chunk and
+        # torch.cat([]) raises (rendering.py:150-161)
+        raise ValueError("nerf_pl_amd.render_rays: empty ray batch (the reference's "
+                         "inference() concatenates an empty chunk list, rendering.py:161)")
     rng = PhiloxRNG() if rng is None else rng
     seed = rng.seed
 
