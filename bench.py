@@ -559,7 +559,9 @@ def main():
         opt = FusedAdam(params, lr=5e-4, eps=1e-8)
         if world > 1:
             from nerf_pl_amd.distributed import GradAllReducer
-            reducer = GradAllReducer(params)
+            # one bucket per model: the fine model's all-reduce overlaps the
+            # coarse model's backward
+            reducer = GradAllReducer(params, buckets=[list(m.parameters()) for m in wl["models"]])
 
     def step():
         loss = wl["step"]()
@@ -567,7 +569,7 @@ def main():
             opt.zero_grad(set_to_none=True)
             loss.backward()
             if reducer is not None:
-                reducer()            # one RCCL all-reduce of the 4.77 MB gradient
+                reducer()            # waits for the RCCL all-reduces of the 4.77 MB gradient
             opt.step()
         return loss
 

@@ -3,52 +3,118 @@
 Rays are independent, so each rank renders its own ray batch and the only
 collective is the gradient all-reduce that Lightning's DDP backend performs in
 the reference (train.py:174-175): 2 x 595,844 fp32 parameters = 4.77 MB per
-step.  Here it is ONE flat all-reduce (RCCL over xGMI with the ``nccl``
-backend on ROCm; gloo on CPU for tests) instead of DDP's per-bucket hooks --
-at 4.77 MB a single ring all-reduce is already latency-bound (tens of µs).
+step.  Here it is one flat all-reduce per model (RCCL over xGMI with the
+``nccl`` backend on ROCm; gloo on CPU for tests) instead of DDP's 25 MB
+buckets: at 4.77 MB a ring all-reduce is latency-bound (tens of µs), so the
+buckets are coarse -- one per model, the fine model's overlapped with the
+coarse model's backward.
 """
 from __future__ import annotations
+
+import functools
 
 import torch
 import torch.distributed as dist
 
 
+class _Bucket:
+    def __init__(self, params, dev):
+        self.params = params
+        self.flat = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=dev)
+        self.views, off = [], 0
+        for p in params:
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        self.seen = set()
+        self.handle = None
+        self.stale = False
+
+
 class GradAllReducer:
     """Averages the ``.grad`` of ``params`` over the default process group.
 
-    Gradients are gathered into one persistent flat buffer (one batched
-    ``cat`` launch), all-reduced once (``AVG`` on RCCL; ``SUM`` and a scale on
-    gloo, which has no average) and scattered back with one batched foreach
-    copy -- a handful of launches per step instead of two per tensor.
-    Parameters without a gradient on every rank are treated as zero (they
-    contribute nothing to the sum), matching DDP's ``find_unused_parameters``
-    behaviour for a fixed graph."""
+    ``buckets`` (optional) partitions the parameters, e.g. one bucket per
+    model: a bucket's all-reduce is started from a post-accumulate-grad hook
+    as soon as the last of its gradients has been accumulated, so it runs on
+    RCCL's stream while the rest of the backward pass is still computing.  In
+    ``render_rays`` the fine model's backward completes first (autograd runs
+    the later-created graph first), so its 2.38 MB all-reduce hides behind the
+    coarse model's backward; only the coarse model's remains exposed.  Without
+    ``buckets`` all parameters form one bucket (the all-reduce starts when the
+    whole backward is done).
 
-    def __init__(self, params, group=None):
+    Per bucket: one batched ``cat`` into a persistent flat buffer, one
+    all-reduce (``AVG`` on RCCL; ``SUM`` and a scale on gloo, which has no
+    average), one batched foreach copy back.  Parameters without a gradient
+    are treated as zero (they contribute nothing to the sum), like DDP's
+    ``find_unused_parameters`` for a fixed graph.  A gradient accumulated
+    again after its bucket was launched (a model used twice, or several
+    backward passes before the call) marks the bucket stale: ``__call__`` then
+    reduces it again from the final gradients.  Every rank must run the same
+    graph (the same buckets complete in the same order), as with DDP."""
+
+    def __init__(self, params, group=None, buckets=None):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
-        n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.views = []
-        off = 0
-        for p in self.params:
-            self.views.append(self.flat[off:off + p.numel()].view_as(p))
-            off += p.numel()
+        if buckets is None:
+            groups = [self.params]
+        else:
+            ids = {id(p) for p in self.params}
+            groups, seen = [], set()
+            for b in buckets:
+                g = [p for p in b if id(p) in ids and id(p) not in seen]
+                seen.update(id(p) for p in g)
+                if g:
+                    groups.append(g)
+            rest = [p for p in self.params if id(p) not in seen]
+            if rest:
+                groups.append(rest)
+        self.buckets = [_Bucket(g, dev) for g in groups]
+        self._hooks = [p.register_post_accumulate_grad_hook(functools.partial(self._ready, b))
+                       for b in self.buckets for p in b.params]
+
+    def _nccl(self):
+        return dist.get_backend(self.group) == "nccl"
+
+    def _ready(self, b, p):
+        if b.handle is not None:
+            b.stale = True
+            return
+        b.seen.add(id(p))
+        if len(b.seen) == len(b.params):
+            self._launch(b)
+
+    def _launch(self, b):
+        for p in b.params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        torch.cat([p.grad.reshape(-1) for p in b.params], out=b.flat)
+        op = dist.ReduceOp.AVG if self._nccl() else dist.ReduceOp.SUM
+        b.handle = dist.all_reduce(b.flat, op=op, group=self.group, async_op=True)
 
     def __call__(self):
         world = dist.get_world_size(self.group)
-        for p in self.params:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-        grads = [p.grad for p in self.params]
-        torch.cat([g.reshape(-1) for g in grads], out=self.flat)
-        if dist.get_backend(self.group) == "nccl":
-            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=self.group)
-        else:
-            dist.all_reduce(self.flat, group=self.group)
-            self.flat.div_(world)
-        torch._foreach_copy_(grads, self.views)
+        for b in self.buckets:
+            if b.handle is not None and b.stale:
+                b.handle.wait()
+                b.handle = None
+            if b.handle is None:
+                self._launch(b)
+        for b in self.buckets:
+            b.handle.wait()
+            if not self._nccl():
+                b.flat.div_(world)
+            torch._foreach_copy_([p.grad for p in b.params], b.views)
+            b.seen.clear()
+            b.handle = None
+            b.stale = False
+
+    def remove(self):
+        """Detach the gradient hooks."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
 
 
 def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None):

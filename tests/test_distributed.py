@@ -67,6 +67,71 @@ def test_grad_allreduce_matches_single_process():
         assert torch.all(ug == 0)
 
 
+def _bucket_worker(rank, world, port, q):
+    """two models in separate buckets, reducer built before backward (the
+    buckets launch from the gradient hooks); model b is used twice in the loss
+    and a second backward accumulates before the call (stale buckets)"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nerf_pl_amd.distributed import GradAllReducer
+        ma, mb, x_all, y_all = _two_models()
+        red = GradAllReducer(list(ma.parameters()) + list(mb.parameters()),
+                             buckets=[list(ma.parameters()), list(mb.parameters())])
+        x, y = x_all[rank::world], y_all[rank::world]
+        out = []
+        for it in range(2):
+            for m in (ma, mb):
+                m.zero_grad(set_to_none=True)
+            for _ in range(1 + it):          # it 1: two backward passes accumulate
+                _two_model_loss(ma, mb, x, y).backward()
+            red()
+            # numpy: pickled by value (tensors would be shared through file
+            # descriptors that die with this process)
+            out.append([p.grad.numpy().copy() for p in list(ma.parameters()) + list(mb.parameters())])
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _two_models():
+    torch.manual_seed(1)
+    ma = torch.nn.Sequential(torch.nn.Linear(5, 6), torch.nn.ReLU(), torch.nn.Linear(6, 3))
+    mb = torch.nn.Linear(5, 3)
+    g = torch.Generator().manual_seed(7)
+    return ma, mb, torch.randn(8, 5, generator=g), torch.randn(8, 3, generator=g)
+
+
+def _two_model_loss(ma, mb, x, y):
+    return ((ma(x) - y) ** 2).mean() + ((mb(x) + mb(2 * x) - y) ** 2).mean()
+
+
+def test_bucketed_allreduce_overlapped_from_hooks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ma, mb, x_all, y_all = _two_models()
+    for it in range(2):
+        for m in (ma, mb):
+            m.zero_grad(set_to_none=True)
+        loss = sum(_two_model_loss(ma, mb, x_all[r::world], y_all[r::world])
+                   for r in range(world)) / world * (1 + it)
+        loss.backward()
+        ref = [p.grad for p in list(ma.parameters()) + list(mb.parameters())]
+        for rank, out in res:
+            for a, b in zip(out[it], ref):
+                torch.testing.assert_close(torch.from_numpy(a), b, rtol=1e-6, atol=1e-7)
+
+
 def _shard_worker(rank, world, port, q, n):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
