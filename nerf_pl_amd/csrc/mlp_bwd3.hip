@@ -213,8 +213,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         const int S = g;
         f32x4 v = {S ? dzr[1][0] : dzr[0][0], S ? dzr[1][1] : dzr[0][1],
                    S ? dzr[1][2] : dzr[0][2], S ? dsig[1] : dsig[0]};
-#if NR_BF1     // bf16 [block][32 samples][4] at the fp32 block stride (wgrad.hip's head DMA)
-        *reinterpret_cast<u32x2*>(reinterpret_cast<char*>(GD + nr_gd_dhead(nb) + (size_t)blk * 128) +
+#if NR_BF1     // bf16 [block][32 samples][4], 256 B per block (wgrad.hip's head DMA)
+        *reinterpret_cast<u32x2*>(reinterpret_cast<char*>(GD + nr_gd_dhead(nb) + (size_t)blk * 64) +
                                   (16 * S + (lane & 15)) * 8) = pack_bf16x4(v);
 #else
         *reinterpret_cast<f32x4*>(GD + nr_gd_dhead(nb) + ((size_t)blk * 32 + 16 * S + (lane & 15)) * 4) = v;
@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     NoSide none;
     NoNext nonext;
     ZeroInit zero;
-    auto dzseg = [&](int l) { return GD + nr_gd_dz(l, nb) + (size_t)blk * NR_NATIVE(256); };
+    auto dzseg = [&](int l) { return GD + nr_gd_dz(l, nb) + (size_t)blk * NR_SEGF(256); };
     auto mwords = [&](int l, uint32_t (&w)[4]) {
         const uint4 m = mask[l * 64];
         w[0] = m.x; w[1] = m.y; w[2] = m.z; w[3] = m.w;
@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     mwords(ML, NAME.mw);
 
     // d feat = W_dir[:, :256]^T dz_dir (xyz_encoding_final has no activation); stores dz_dir
-    GradU<8, false> uc{C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_NATIVE(128), {0u, 0u, 0u, 0u},
+    GradU<8, false> uc{C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_SEGF(128), {0u, 0u, 0u, 0u},
                        lane};
     GradU<16, false> ua{A, dzseg(8), {0u, 0u, 0u, 0u}, lane};     // dfeat
     // f16x3: the sigma head injects w_sigma dsigma (|.| <= max|w_sigma| |dsigma|)

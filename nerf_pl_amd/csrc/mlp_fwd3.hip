@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 
     Act A, B;
     Pieces b[2];       // pieces of the next k-step
-    auto hseg = [&](int l) { return SV + nr_sv_h(l, nb) + (size_t)blk * NR_NATIVE(256); };
+    auto hseg = [&](int l) { return SV + nr_sv_h(l, nb) + (size_t)blk * NR_SEGF(256); };
     auto mseg = [&](int l) {
         return reinterpret_cast<uint32_t*>(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + l) * 256;
     };
@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     split_all(peu, b);
     U u1{A, hseg(0), mseg(0), nullptr, lane, g};
     {
-        PeSide<SAVE> side{pe, SV + (size_t)blk * NR_NATIVE(64), g, lane};
+        PeSide<SAVE> side{pe, SV + (size_t)blk * NR_SEGF(64), g, lane};
         auto bi = bias(NR_H_BIAS(1));
         segment<FwdTab, kL1, 2, 2, QEND, true>(dma, lane, A, peu, u1, bi, side, b, f0);
     }
@@ -424,7 +424,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             }
         PeU<8> dpeu{dpe};
         // xyz_encoding_final: no activation (nerf.py:116)
-        AccU<false, SAVE, false, false> uf{A, SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256),
+        AccU<false, SAVE, false, false> uf{A, SV + nr_sv_feat(nb) + (size_t)blk * NR_SEGF(256),
                                            nullptr, nullptr, lane, g};
         { auto bi = bias(NR_H_BFINAL); segment<FwdTab, kFinal, 8, 2, QEND, true>(dma, lane, A, u8, uf, bi, none, b, f0); }
         NR_STAMP(11);
@@ -439,7 +439,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         f32x4 C[8][2];
         { auto bi = bias(NR_H_BDIR); segment<FwdTab, kDir, 8, 1, QEND, true>(dma, lane, C, uf, dpeu, bi, none, b, f0); }
         {   // PE(dir) part (stores the dir PE slots)
-            DirPeSide<SAVE> side{dpe, SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32), g, lane};
+            DirPeSide<SAVE> side{dpe, SV + nr_sv_dirpe(nb) + (size_t)blk * NR_SEGF(32), g, lane};
             segment<FwdTab, kDir + 8, 1, 1, QEND, false>(dma, lane, C, dpeu, nonext, zero, side, b, f0);
         }
         NR_STAMP(12);
@@ -466,7 +466,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         }
 #endif
         if constexpr (SAVE) {
-            float* hd = SV + nr_sv_hdir(nb) + (size_t)blk * NR_NATIVE(128);
+            float* hd = SV + nr_sv_hdir(nb) + (size_t)blk * NR_SEGF(128);
             uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int F = 0; F < 8; ++F)

@@ -360,8 +360,8 @@ struct Stager {
             v0 = p[0]; v1 = p[1];
         } else {
             constexpr int F4 = Geo3<KIND, W>::CHUNKS * 64;
-#if NR_BF1      // bf16 segments (x3.h store_slot): 8-B slots, sample-major chunks, fp32 block stride
-            const x3::u32x2* p = reinterpret_cast<const x3::u32x2*>(base) + (size_t)blk * 2 * F4 +
+#if NR_BF1      // bf16 segments (x3.h store_slot): 8-B slots, sample-major chunks, NR_SEGF block stride
+            const x3::u32x2* p = reinterpret_cast<const x3::u32x2*>(base) + (size_t)blk * F4 +
                                  x3::bf16_slot(Geo3<KIND, W>::f4(k, h, hb, 2 * jp));
             v0 = x3::unpack_bf16x4(p[0]); v1 = x3::unpack_bf16x4(p[4]);
 #else
@@ -783,7 +783,7 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
     // the resources start at this workgroup's first block: buffer offsets and
     // sizes are 32-bit, and a whole segment passes 2^31 bytes at 2^16 blocks
     // (2.1M samples per call) while one workgroup's slice stays far below
-    constexpr int64_t ABLK = HEADA ? 512 : WA * 128, BBLK = WB * 128;
+    constexpr int64_t ABLK = HEADA ? 256 : WA * 64, BBLK = WB * 64;   // bytes per block (NR_SEGF)
     const int nblk = b1_ - b0;
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(reinterpret_cast<const char*>(T.a.base) + (int64_t)b0 * ABLK), 0, (int)(nblk * ABLK), 0x00020000);
@@ -799,10 +799,10 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
             const int t = isa ? i : i - TA;
             auto* dst = (__attribute__((address_space(3))) void*)(img + (isa ? i * kTile : ABYTES + t * kTile));
             if (HEADA && isa)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 4, lane * 4, b * 512, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 4, lane * 4, b * 256, 0, 0);
             else
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(isa ? ra : rb, dst, 16, lane * 16,
-                                                         b * (isa ? WA : WB) * 128 + t * 1024, 0, 0);
+                                                         b * (isa ? WA : WB) * 64 + t * 1024, 0, 0);
         }
     };
     f32x16 acc[MT][NT];

@@ -538,9 +538,18 @@ __device__ __forceinline__ float acc_b(const f32x4 (&X)[NF][2], int s, int sb, i
 // rows of 32 B.  One wave store still covers the chunk's contiguous 512 B,
 // and wgrad.hip's LDS-DMA copies chunks as they are and reads its MFMA
 // fragments with ds_read_b64_tr_b16 (one 4-sample x 16-feature block per
-// 16 lanes).  Segments keep the fp32 block stride (buffers keep their sizes
-// and offsets), so a block uses the first half of its fp32 footprint.
+// 16 lanes).  Blocks are packed at half the fp32 block stride (NR_SEGF):
+// segments keep their fp32 offsets and sizes inside the buffers, and a
+// segment's blocks fill the first half of it contiguously -- at the fp32
+// stride every read skipped every other 16 KiB, which left the weight
+// gradient's stream at 58% of HBM bandwidth.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// floats from one block of a width-w saved segment to the next
+#if NR_BF1
+#define NR_SEGF(w) (NR_NATIVE(w) / 2)
+#else
+#define NR_SEGF(w) NR_NATIVE(w)
+#endif
 __device__ __forceinline__ u32x2 pack_bf16x4(const f32x4& v) {
     const bf16x2 a = __builtin_convertvector((f32x2){v[0], v[1]}, bf16x2);
     const bf16x2 b = __builtin_convertvector((f32x2){v[2], v[3]}, bf16x2);
