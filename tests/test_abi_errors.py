@@ -83,3 +83,12 @@ def test_python_wrapper_raises_with_message():
     from nerf_pl_amd import _lib
     with pytest.raises(RuntimeError, match=r"nr_embed failed \(code 10001\): nr_embed: bad sizes"):
         _lib.call("nr_embed", None, -1, 10, None, None)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No fallback: without the built library every entry point raises."""
+    from nerf_pl_amd import _lib
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libnerf_pl_amd.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(RuntimeError, match="HIP library not built"):
+        _lib.call("nr_embed", None, 0, 10, None, None)
