@@ -4,5 +4,5 @@
 set -e
 name=$1; shift
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize --offload-arch=gfx950 \
-  -DNR_F16=1 "$@" -shared -o dev/libh3_$name.so nerf_pl_amd/csrc/mlp_fwd3.hip \
+  -DNR_F16=${NR_F16:-1} "$@" -shared -o dev/libh3_$name.so nerf_pl_amd/csrc/mlp_fwd3.hip \
   nerf_pl_amd/csrc/mlp_bwd3.hip nerf_pl_amd/csrc/wgrad.hip nerf_pl_amd/csrc/errors.hip

@@ -1,5 +1,6 @@
 """Time f16x3 kernel variants built by dev/h3var.sh at the cfg2 fine-pass size
-(dev only): python dev/time_h3var.py base,nt,... [reps]"""
+(dev only): python dev/time_h3var.py base,nt,... [reps]
+NR_VAR_MATH=bf16 times plain-bf16 variants (built with -DNR_F16=0 -DNR_BF1=1)."""
 import ctypes
 import os
 import sys
@@ -14,7 +15,9 @@ from nerf_pl_amd.functions import _wgrad_workspace  # noqa: E402
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)
 flat = (torch.rand(packing.N_PARAMS, device=dev) - 0.5) * 0.15
-ph, pbh = ops.pack_fwd3(flat, math="f16x3"), ops.pack_bwd(flat, math="f16x3")
+MATH = os.environ.get("NR_VAR_MATH", "f16x3")
+SFX, NP = {"f16x3": ("_h3", 2), "bf16": ("_b1", 1)}[MATH]
+ph, pbh = ops.pack_fwd3(flat, math=MATH), ops.pack_bwd(flat, math=MATH)
 n_rays, spr = 4096, 192
 n = n_rays * spr
 rays = torch.randn(n_rays, 8, device=dev)
@@ -32,14 +35,16 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 ref = None
 for v in sys.argv[1].split(","):
     L = ctypes.CDLL(os.path.abspath(f"dev/libh3_{v}.so"))
-    f, b, w = L.nr_mlp_fwd_h3, L.nr_mlp_bwd_h3, L.nr_wgrad_h3
+    f, b, w = (getattr(L, "nr_mlp_fwd" + SFX), getattr(L, "nr_mlp_bwd" + SFX),
+               getattr(L, "nr_wgrad" + SFX))
+    pk, pkb = getattr(L, "nr_pack" + SFX), getattr(L, "nr_pack_bwd" + SFX)
     # weights packed by the variant itself (its weight scale may differ)
-    L.nr_pack_h3.argtypes = [P, P, I64, P, P, P]
-    L.nr_pack_bwd_h3.argtypes = [P, P, I64, P, P]
-    m, hm = ops._maps3(0, 2)
-    mb = ops._map_bwd3(0, 2)
-    assert L.nr_pack_h3(flat.data_ptr(), m.data_ptr(), m.numel(), hm.data_ptr(), ph.data_ptr(), st) == 0
-    assert L.nr_pack_bwd_h3(flat.data_ptr(), mb.data_ptr(), mb.numel(), pbh.data_ptr(), st) == 0
+    pk.argtypes = [P, P, I64, P, P, P]
+    pkb.argtypes = [P, P, I64, P, P]
+    m, hm = ops._maps3(0, NP)
+    mb = ops._map_bwd3(0, NP)
+    assert pk(flat.data_ptr(), m.data_ptr(), m.numel(), hm.data_ptr(), ph.data_ptr(), st) == 0
+    assert pkb(flat.data_ptr(), mb.data_ptr(), mb.numel(), pbh.data_ptr(), st) == 0
     f.argtypes = [P, P, P, I64, I, P, I, I, P, P, P]
     b.argtypes = [P, P, P, P, P, I64, P, P]
     w.argtypes = [P, P, I64, P, P, P]

@@ -21,6 +21,10 @@ constexpr int kLdsBytes = kRingBytes + kMaskBytes + kHeadDma * 1024;
 
 struct BwdTab {
     __host__ __device__ static constexpr int64_t off(int q) { return (int64_t)q * kSlotBytes; }
+    // merged ring (x3.h): every transposed layer has two input halves per k-step
+    __host__ __device__ static constexpr int sg(int q) { return q / 2; }
+    __host__ __device__ static constexpr int first(int G) { return 2 * G; }
+    __host__ __device__ static constexpr int size(int) { return 2; }
 };
 static_assert(BwdTab::off(kQ) == (NR_F16 ? 2228224 : (NR_BF1 ? 1114112 : 3342336)),
               "packed size must match packing.BWD3_BYTES");
@@ -199,7 +203,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     const uint4* mask = smask + lane;                   // [layer * 64]
     const float* H = Hs;
     Frag f0;                                            // tile-0 fragments of the next k-group
-    enter<0, kQ>(smem, lane, f0);
+    enter<BwdTab, 0, kQ>(smem, lane, f0);
 
     float dzr[2][3], dsig[2];
 #pragma unroll

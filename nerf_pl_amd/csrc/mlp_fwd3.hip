@@ -38,6 +38,11 @@ struct FwdTab {
     __host__ __device__ static constexpr int64_t off(int q) {
         return (int64_t)kHeadBytes + (int64_t)q * kSlotBytes;
     }
+    // merged ring (x3.h): the 256-wide layers' k-steps pair their two output
+    // halves; the dir layer's groups (one half) stand alone
+    __host__ __device__ static constexpr int sg(int q) { return q < kDir ? q / 2 : kDir / 2 + (q - kDir); }
+    __host__ __device__ static constexpr int first(int G) { return G < kDir / 2 ? 2 * G : kDir + (G - kDir / 2); }
+    __host__ __device__ static constexpr int size(int G) { return G < kDir / 2 ? 2 : 1; }
 };
 static_assert(FwdTab::off(kQAll) == (NR_F16 ? 2388000 : (NR_BF1 ? 1200160 : 3575840)),
               "packed size must match packing.fwd3_offsets()");
@@ -342,7 +347,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     NR_STAMP(0);       // inputs + positional encoding
 
     Frag f0;           // tile-0 fragments of the next k-group
-    enter<0, QEND>(smem, lane, f0);
+    enter<FwdTab, 0, QEND>(smem, lane, f0);
     NR_STAMP(1);       // prologue: + first weight group
 
     Act A, B;

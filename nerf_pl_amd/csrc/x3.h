@@ -119,25 +119,76 @@ constexpr int kTiles = 8;                          // output tiles (16 rows) per
 #endif
 constexpr int kSlots = NR_X3_SLOTS;
 constexpr int kSlotBytes = kNP * kTiles * 1024;    // pieces x 8 tiles x 1 KiB
-constexpr int kRingBytes = kSlots * kSlotBytes;
 constexpr int kDma = kNP * kTiles / kWaves;        // DMA instructions per wave per group
+// Merged ring (NR_X3_MERGE): the groups of one k-step (both output halves of a
+// 256-wide layer) share one ring slot of 2 groups and ONE hand-over (wait +
+// barrier) instead of one per group; the packed layout is unchanged (the two
+// halves are adjacent).  TAB::sg(q) maps group q to its k-step ("super-group"),
+// TAB::first(G) / TAB::size(G) give a super-group's first group and group
+// count.  The DMA of super-group G + kSS - 1 is issued during G.  Halves the
+// barriers of the 256-wide layers (dev/mb_w8.hip "32 KiB groups").
+#ifndef NR_X3_MERGE
+#define NR_X3_MERGE (NR_F16 || NR_BF1)
+#endif
+constexpr bool kMerge = NR_X3_MERGE;
+#ifndef NR_X3_SSLOTS
+#define NR_X3_SSLOTS (NR_F16 ? 3 : (NR_BF1 ? 6 : 2))
+#endif
+constexpr int kSS = NR_X3_SSLOTS;                  // super-slots of the merged ring
+// the DMA issued during super-group G must be for G + 2 or later: for G + 1
+// (kSS = 2) the hand-over's vmcnt, which leaves the current half's stores in
+// flight, can leave that DMA's last instructions in flight too (measured: a
+// run-to-run gradient difference)
+static_assert(!kMerge || kSS >= 3, "merged ring needs >= 3 super-slots");
+constexpr int kSuperBytes = 2 * kSlotBytes;
+constexpr int kRingBytes = kMerge ? kSS * kSuperBytes : kSlots * kSlotBytes;
 
 template <int V> using IC = std::integral_constant<int, V>;
 
 typedef f32x4 Act[16][2];                      // 256-wide activation of one wave
 
 // vm operations this wave issued after its DMA for group q by the time group
-// q is consumed: the DMA of the kSlots-2 groups after it (stores only add,
-// so the count is a safe lower bound)
-template <int Q, int QEND>
+// q is consumed: the DMA of the kSlots-2 groups after it (merged ring: of the
+// kSS-2 super-groups after q's) -- stores only add, so the count is a safe
+// lower bound
+template <class TAB, int Q, int QEND>
 __host__ __device__ constexpr int wait_count() {
     int n = 0;
-    for (int k = Q + 1; k <= Q + kSlots - 2; ++k)
-        if (k < QEND) n += kDma;
+    if constexpr (kMerge) {
+        const int G = TAB::sg(Q);
+        for (int H = G + 1; H <= G + kSS - 2; ++H)
+            for (int q = TAB::first(H); q < TAB::first(H) + TAB::size(H); ++q)
+                if (q < QEND) n += kDma;
+    } else {
+        for (int k = Q + 1; k <= Q + kSlots - 2; ++k)
+            if (k < QEND) n += kDma;
+    }
     return n;
 }
 
-__device__ __forceinline__ char* slot_ptr(char* ring, int q) { return ring + (q % kSlots) * kSlotBytes; }
+// LDS byte offset of group Q's ring slot
+template <class TAB, int Q>
+__host__ __device__ constexpr int slot_off() {
+    if constexpr (kMerge)
+        return (TAB::sg(Q) % kSS) * kSuperBytes + (Q - TAB::first(TAB::sg(Q))) * kSlotBytes;
+    else
+        return (Q % kSlots) * kSlotBytes;
+}
+
+// the group whose DMA instructions run during group Q (>= QEND: none).  Merged:
+// position p of super-group G feeds position p of G + kSS - 1 (super-group
+// sizes never grow along a kernel's sequence, checked here)
+template <class TAB, int Q, int QEND>
+__host__ __device__ constexpr int dma_target() {
+    if constexpr (kMerge) {
+        constexpr int G = TAB::sg(Q), p = Q - TAB::first(G), G2 = G + kSS - 1;
+        static_assert(TAB::first(G2) >= QEND || TAB::size(G2) <= TAB::size(G),
+                      "merged ring: a super-group larger than the one issuing its DMA");
+        return p < TAB::size(G2) ? TAB::first(G2) + p : (1 << 30);
+    } else {
+        return Q + kSlots - 1;
+    }
+}
 
 // LDS-DMA of the packed weights: buffer_load_dwordx4 ... lds with a scalar
 // byte offset (group offset + fragment) and the lane's 16 B in voffset, the
@@ -165,7 +216,7 @@ __device__ __forceinline__ void dma_one(const Dma& d, int k) {
     if constexpr (Q < QEND && NR_X3_DBG != 3) {
         const int i = d.wave + kWaves * k;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            d.rsrc, (__attribute__((address_space(3))) void*)(slot_ptr(d.ring, Q) + i * 1024), 16,
+            d.rsrc, (__attribute__((address_space(3))) void*)(d.ring + slot_off<TAB, Q>() + i * 1024), 16,
             d.voff, (int)TAB::off(Q) + i * 1024, 0, 0);
     }
 }
@@ -176,10 +227,11 @@ __device__ __forceinline__ void stage(const Dma& d) {
     for (int k = 0; k < kDma; ++k) dma_one<TAB, Q, QEND>(d, k);
 }
 
-// stages groups 0 .. kSlots-2
+// stages groups 0 .. kSlots-2 (merged: super-groups 0 .. kSS-2)
 template <class TAB, int QEND, int Q = 0>
 __device__ __forceinline__ void prologue(const Dma& d) {
-    if constexpr (Q < kSlots - 1) {
+    constexpr int LIM = kMerge ? TAB::first(kSS - 1) : kSlots - 1;
+    if constexpr (Q < LIM) {
         stage<TAB, Q, QEND>(d);
         prologue<TAB, QEND, Q + 1>(d);
     }
@@ -189,10 +241,10 @@ __device__ __forceinline__ void prologue(const Dma& d) {
 // vmcnt retires in issue order (loads, stores and LDS-DMA together), so the
 // EXTRA stores issued after group Q's DMA in the current group are left in
 // flight too; older stores are waited for (they have had a group to land).
-template <int Q, int QEND, int EXTRA = 0>
+template <class TAB, int Q, int QEND, int EXTRA = 0>
 __device__ __forceinline__ void ring_enter() {
     if constexpr (NR_X3_DBG < 2)
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(wait_count<Q, QEND>() + EXTRA) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(wait_count<TAB, Q, QEND>() + EXTRA) : "memory");
     if constexpr (NR_X3_DBG == 0) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
@@ -286,19 +338,22 @@ __device__ __forceinline__ float relu_i(float x) {
 // the weight pieces of one output tile of a k-group
 struct Frag { p8 p[kNP]; };
 
-template <int Q>
+template <class TAB, int Q>
 __device__ __forceinline__ void rd_frag(char* ring, int lane, int t, Frag& f) {
-    const char* s = slot_ptr(ring, Q) + lane * 16 + t * 1024;
+    const char* s = ring + slot_off<TAB, Q>() + lane * 16 + t * 1024;
 #pragma unroll
     for (int k = 0; k < kNP; ++k) f.p[k] = *reinterpret_cast<const p8*>(s + k * kTiles * 1024);
 }
 
-// hand group Q over (wait + barrier) and read its tile-0 fragments
-template <int Q, int QEND, int EXTRA = 0>
+// hand group Q over (wait + barrier) and read its tile-0 fragments; in the
+// merged ring a group that shares its predecessor's super-group arrived with
+// it, and only its tile-0 fragments are read
+template <class TAB, int Q, int QEND, int EXTRA = 0>
 __device__ __forceinline__ void enter(char* ring, int lane, Frag& f0) {
     if constexpr (Q < QEND) {
-        ring_enter<Q, QEND, EXTRA>();
-        rd_frag<Q>(ring, lane, 0, f0);
+        if constexpr (!(kMerge && Q > 0 && TAB::sg(Q) == TAB::sg(Q - 1)))
+            ring_enter<TAB, Q, QEND, EXTRA>();
+        rd_frag<TAB, Q>(ring, lane, 0, f0);
     }
 }
 
@@ -367,10 +422,10 @@ __device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][
 #pragma unroll
     for (int t = 0; t < kTiles; ++t) {
         if (t + 1 < kTiles) {
-            rd_frag<Q>(ring, lane, t + 1, f[(t + 1) & 1]);
+            rd_frag<TAB, Q>(ring, lane, t + 1, f[(t + 1) & 1]);
             if constexpr (INIT) { ci[(t + 1) & 1][0] = cinit(F0 + t + 1, 0); ci[(t + 1) & 1][1] = cinit(F0 + t + 1, 1); }
         }
-        if (t == kTiles - 1) enter<Q + 1, QEND, EXTRA>(ring, lane, f0);
+        if (t == kTiles - 1) enter<TAB, Q + 1, QEND, EXTRA>(ring, lane, f0);
         __builtin_amdgcn_sched_barrier(0);
         f32x4& d0 = acc[F0 + t][0];
         f32x4& d1 = acc[F0 + t][1];
@@ -470,7 +525,7 @@ __device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)
     if constexpr (HF < NH) {
         constexpr int Q = Q0 + NH * S + HF;
         auto hook = [&](int t) {
-            if (t < kDma) dma_one<TAB, Q + kSlots - 1, QEND>(dma, t);
+            if (t < kDma) dma_one<TAB, dma_target<TAB, Q, QEND>(), QEND>(dma, t);
             const int u = unit_at<NH, HF>(t);
             if (u >= 0) {
                 if constexpr (S + 1 < KS) split_unit(getu, IC<S + 1>(), u, bn);
