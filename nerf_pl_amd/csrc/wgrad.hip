@@ -35,12 +35,13 @@ enum SegKind { SEG_ACC = 0, SEG_PE = 1, SEG_DPE = 2, SEG_HEAD = 3 };
 // f16x3: the task pairs that read the same saved segment (wgrad_launch:
 // DZ(4), H(7), dz_dir) run fused -- one workgroup stages the shared segment
 // once and computes both outputs.  Runtime switch NR_WGRAD_FUSE=0 (host).
-constexpr bool kFuse = NR_F16;   // (bf16: the LDS-DMA body below reads every segment once per task)
+constexpr bool kFuse = NR_F16 || NR_BF1;
 #ifndef NR_WG_PE_WM
 #define NR_WG_PE_WM 4            // wave grid rows of the fused PE output (256 x 64)
 #endif
 #ifndef NR_WGRAD_FUSE_MASK
-#define NR_WGRAD_FUSE_MASK 7     // bit i: pair i of wgrad_launch's kFused (6: no spills, measured slower)
+// bit i: pair i of wgrad_launch's kFused (f16x3 6: no spills, measured slower)
+#define NR_WGRAD_FUSE_MASK 7
 #endif
 
 // flat parameter offsets, NeRF.named_parameters() order (packing.py param_offsets)
@@ -722,14 +723,17 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
 namespace b1 {
 constexpr int kTile = 1152;      // LDS bytes per 16-feature tile of a block
 constexpr int kDepth = 4;        // blocks in the ring
-constexpr int kLds = kDepth * 32 * kTile;   // 256 + 256 features
+// the whole LDS: 256 + 256 features per block (+ a fused task's extra operand)
+constexpr int kLds = 160 * 1024;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 // fragment rows r0 .. r0+31 (features), k-step S (samples 16S .. 16S+15) of a block image
+// (TS: the image's tile stride -- kTile, or 1024 for an unpadded extra operand)
+template <int TS = kTile>
 __device__ __forceinline__ x3::p8 frag_tr(const char* img, int r0, int S, int lane) {
     const int g4 = lane >> 4, i = lane & 15;
-    const char* p = img + ((r0 >> 4) + (g4 & 1)) * kTile + S * 512 + 32 * (8 * (g4 >> 1) + (i >> 2)) +
+    const char* p = img + ((r0 >> 4) + (g4 & 1)) * TS + S * 512 + 32 * (8 * (g4 >> 1) + (i >> 2)) +
                     8 * (i & 3);
     typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
@@ -764,17 +768,35 @@ __device__ __forceinline__ float frag_sum(const x3::p8& f) {
 // bf16 [block][32 samples][4] (mlp_bwd3.hip): one 256-B dword LDS-DMA per
 // block, and every lane of a transposed read points at its sample's 4 values
 // (rows 4 .. 31 of the fragment repeat them and are never written out)
-template <int WA, int WB, int WM, int WN, bool HEADA = false>
+//
+// Fused task pairs (XMODE, as wgrad3_body's extra operand): XMODE 1 -- a
+// second input segment X (XW columns, XW / 16 tiles) shares the gradient
+// operand A; the waves of grid column 0 also compute A x X into the partner's
+// slab `xslab` (dz_dir x [feat | dir PE]).  XMODE 2 -- a second gradient
+// segment, the 4-column head (dword DMA, frag_head), shares the input operand
+// B; the waves of grid row 0 also compute head x B ([dfeat | head] x h8).
+// Either way the shared segment is read once.
+template <int WA, int WB, int WM, int WN, bool HEADA = false, int XMODE = 0, int XW = 0>
 __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, int b0, int b1_,
-                                              char* lds, float* __restrict__ slab) {
+                                              char* lds, float* __restrict__ slab,
+                                              float* __restrict__ xslab = nullptr) {
     using namespace b1;
     static_assert(!HEADA || WA == 4, "head operand");
-    constexpr int TA = HEADA ? 1 : WA / 16, TB = WB / 16, NDMA = TA + TB;
+    static_assert(XMODE == 0 || (!HEADA && (XMODE == 2 || XW % 32 == 0)), "extra operand");
+    constexpr int TA = HEADA ? 1 : WA / 16, TB = WB / 16;
+    constexpr int TX = XMODE == 1 ? XW / 16 : (XMODE == 2 ? 1 : 0);
+    constexpr int NDMA = TA + TB + TX;
     constexpr int ABYTES = HEADA ? 256 : TA * kTile;
-    constexpr int IMG = ABYTES + TB * kTile;
+    constexpr int XOFF = ABYTES + TB * kTile;                       // extra image
+    // the extra operand's tiles go unpadded (2-way bank conflicts on its
+    // fragment reads) when padded ones would not fit the 4-block ring
+    constexpr int XTS = kDepth * (XOFF + TX * kTile) <= b1::kLds ? kTile : 1024;
+    constexpr int IMG = XOFF + (XMODE == 1 ? TX * XTS : (XMODE == 2 ? 256 : 0));
     static_assert(kDepth * IMG <= b1::kLds, "ring");
     constexpr int MT = (WA / WM + 31) / 32, NT = (WB / WN + 31) / 32;
-    constexpr int kWait = (kDepth - 2) * (NDMA / 8);   // this wave's DMAs issued after a block's
+    constexpr int XNT = XMODE == 1 ? XW / 32 : 1;
+    // this wave's DMAs issued after a block's (waves issuing more wait a little longer)
+    constexpr int kWait = (kDepth - 2) * (NDMA / 8);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool active = wave < WM * WN;
@@ -784,25 +806,43 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
     // sizes are 32-bit, and a whole segment passes 2^31 bytes at 2^16 blocks
     // (2.1M samples per call) while one workgroup's slice stays far below
     constexpr int64_t ABLK = HEADA ? 256 : WA * 64, BBLK = WB * 64;   // bytes per block (NR_SEGF)
+    constexpr int64_t XBLK = XMODE == 1 ? XW * 64 : 256;
     const int nblk = b1_ - b0;
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(reinterpret_cast<const char*>(T.a.base) + (int64_t)b0 * ABLK), 0, (int)(nblk * ABLK), 0x00020000);
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(reinterpret_cast<const char*>(T.b.base) + (int64_t)b0 * BBLK), 0, (int)(nblk * BBLK), 0x00020000);
-    // block b -> ring slot: tile i < TA of A, then the TB tiles of B, 1 KiB each
+    const float* xbase = XMODE == 1 ? a.task[T.fuse].b.base : (XMODE == 2 ? a.task[T.fuse].a.base : T.a.base);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(reinterpret_cast<const char*>(xbase) + (int64_t)b0 * XBLK), 0,
+        XMODE ? (int)(nblk * XBLK) : 0, 0x00020000);
+    // block b -> ring slot: tile i < TA of A, then the TB tiles of B, then the
+    // extra operand's tiles (or its 256-B head block), 1 KiB each
     auto dma = [&](int b, int slot) {
         b = min(b, b1_ - 1) - b0; // past the end: re-read the last block (keeps vmcnt exact)
         char* img = lds + slot * IMG;
+        typedef __attribute__((address_space(3))) void* lds_ptr;
+        // one branch per operand (i is wave-uniform): each names its own
+        // buffer resource -- a run-time choice among three put them in scratch
 #pragma unroll
         for (int i = wave; i < NDMA; i += 8) {
-            const bool isa = i < TA;
-            const int t = isa ? i : i - TA;
-            auto* dst = (__attribute__((address_space(3))) void*)(img + (isa ? i * kTile : ABYTES + t * kTile));
-            if (HEADA && isa)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 4, lane * 4, b * 256, 0, 0);
-            else
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(isa ? ra : rb, dst, 16, lane * 16,
-                                                         b * (isa ? WA : WB) * 64 + t * 1024, 0, 0);
+            if (i < TA) {
+                if (HEADA)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)img, 4, lane * 4, b * 256, 0, 0);
+                else
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(img + i * kTile), 16, lane * 16,
+                                                             b * WA * 64 + i * 1024, 0, 0);
+            } else if (i < TA + TB) {
+                const int t = i - TA;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(img + ABYTES + t * kTile), 16,
+                                                         lane * 16, b * WB * 64 + t * 1024, 0, 0);
+            } else if constexpr (XMODE == 2) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr)(img + XOFF), 4, lane * 4, b * 256, 0, 0);
+            } else if constexpr (XMODE == 1) {
+                const int t = i - TA - TB;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr)(img + XOFF + t * XTS), 16,
+                                                         lane * 16, b * XW * 64 + t * 1024, 0, 0);
+            }
         }
     };
     f32x16 acc[MT][NT];
@@ -810,9 +850,24 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
     for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x16{};
+    // extra output: XMODE 1 the (WA/32) x XNT 32x32 tiles dealt to the waves
+    // (tile e = wave + 8k, XTPW per wave); XMODE 2 [1][NT] the head row tile x
+    // B column tiles (grid row 0)
+    constexpr int XRT = WA / 32, XT = XRT * XNT, XTPW = (XT + 7) / 8;
+    static_assert(XMODE != 1 || WA % 32 == 0, "extra tiles");
+    constexpr int XA = XMODE == 1 ? XTPW : 1, XB = XMODE == 2 ? NT : 1;
+    f32x16 xacc[XMODE ? XA : 1][XMODE ? XB : 1];
+    if constexpr (XMODE) {
+#pragma unroll
+        for (int i = 0; i < XA; ++i)
+#pragma unroll
+            for (int j = 0; j < XB; ++j) xacc[i][j] = f32x16{};
+    }
     float bsum[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) bsum[i] = 0.f;
+    float xsum = 0.f;
+    const bool xw = XMODE == 1 ? wave < XT : mi == 0;   // this wave computes extra output
 #pragma unroll
     for (int d = 0; d < kDepth - 1; ++d) dma(b0 + d, d);
 #pragma unroll 1
@@ -835,6 +890,23 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
                 for (int j = 0; j < NT; ++j) acc[i][j] = x3::mfma32(af, bf[j], acc[i][j]);
                 if (ni == 0) bsum[i] += frag_sum(af);
             }
+            if constexpr (XMODE == 1) {
+#pragma unroll
+                for (int k = 0; k < XTPW; ++k) {
+                    const int e = wave + 8 * k;
+                    if (e < XT)
+                        xacc[k][0] = x3::mfma32(frag_tr(img, 32 * (e % XRT), S, lane),
+                                                frag_tr<XTS>(img + XOFF, 32 * (e / XRT), S, lane), xacc[k][0]);
+                }
+            }
+            if constexpr (XMODE == 2) {
+                if (xw) {
+                    const x3::p8 hf = frag_head(img + XOFF, S, lane);
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) xacc[0][j] = x3::mfma32(hf, bf[j], xacc[0][j]);
+                    if (ni == 0) xsum += frag_sum(hf);
+                }
+            }
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's clamped DMAs
@@ -845,7 +917,37 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
         for (int i = 0; i < MT; ++i) {
             const float s = bsum[i] + __shfl_xor(bsum[i], 32);
             const int o = m0 + 32 * i + col;
-            if (h == 0 && o < WA) slab[WA * WB + o] = s;
+            if (h == 0 && o < WA) {
+                slab[WA * WB + o] = s;
+                if constexpr (XMODE == 1) xslab[WA * XW + o] = s;   // shared gradient operand
+            }
+        }
+    }
+    if constexpr (XMODE == 1) {
+#pragma unroll
+        for (int k = 0; k < XTPW; ++k) {
+            const int e = wave + 8 * k;
+            if (e < XT) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    xslab[(32 * (e % XRT) + nr_acc_row(r, h)) * XW + 32 * (e / XRT) + col] = xacc[k][0][r];
+            }
+        }
+    }
+    if constexpr (XMODE == 2) {
+        if (xw) {
+            if (ni == 0) {
+                const float s = xsum + __shfl_xor(xsum, 32);
+                if (h == 0 && col < 4) xslab[4 * WB + col] = s;
+            }
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int o = nr_acc_row(r, h);
+                    const int c = n0 + 32 * j + col;
+                    if (o < 4 && c < WB) xslab[o * WB + c] = xacc[0][j][r];
+                }
         }
     }
 #pragma unroll
@@ -879,6 +981,18 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
     if constexpr (kFuse) if (fu >= 0) {
         const WgTask& P = a.task[fu];
         float* xslab = a.slab + P.slab + (int64_t)c * (P.a.width * P.b.width + P.a.width);
+#if NR_BF1
+        switch (__builtin_amdgcn_readfirstlane(T.id)) {
+#if NR_WGRAD_FUSE_MASK & 1
+            case 5:    // DZ(4) x [H(3) | PE]: xyz_encoding_5 (skip layer)
+                wgrad_b1_body<256, 256, 2, 4, false, 1, 64>(a, T, b0, b1, lds, slab, xslab); break;
+#endif
+            case 9:    // [DZ(8) | head] x H(7): xyz_encoding_final and sigma
+                wgrad_b1_body<256, 256, 2, 4, false, 2, 4>(a, T, b0, b1, lds, slab, xslab); break;
+            case 10:   // dz_dir x [feat | dir PE]: dir_encoding
+                wgrad_b1_body<128, 256, 2, 4, false, 1, 32>(a, T, b0, b1, lds, slab, xslab); break;
+        }
+#else
         switch (__builtin_amdgcn_readfirstlane(T.id)) {
 #if NR_WGRAD_FUSE_MASK & 1
             case 5:    // DZ(4) x [H(3) | PE]: xyz_encoding_5 (skip layer)
@@ -896,6 +1010,7 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
                     a, T, b0, b1, lds, slab, xslab); break;
 #endif
         }
+#endif
         return;
     }
 #if NR_BF1
