@@ -562,6 +562,9 @@ def main():
             # one bucket per model: the fine model's all-reduce overlaps the
             # coarse model's backward
             reducer = GradAllReducer(params, buckets=[list(m.parameters()) for m in wl["models"]])
+            # first collective on the main thread: the communicator is set up
+            # here, not inside the first gradient hook (autograd's thread)
+            dist.barrier()
 
     def step():
         loss = wl["step"]()
