@@ -7,7 +7,10 @@
 // third ("What the layers' remaining ~25% is").
 // STORE 0: no saving stores; 1: every activation saved (1 KiB per dwordx4
 // wave store) + ReLU mask bits, as in training.  8 layers of 256 -> 256.
+// MB_NP=1: the plain-bf16 loop instead (one bf16 piece, one MFMA per product,
+// 8 KiB groups: LDS demand 2x f16x3's per MFMA cycle).
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -fno-slp-vectorize dev/mb_s3.hip -o dev/mb_s3
+//   hipcc ... -DMB_NP=1 dev/mb_s3.hip -o dev/mb_s3_b1
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -18,7 +21,12 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kSlots = 4, kSlotBytes = 16384, kGroups = 16;   // k-groups per layer
+#ifndef MB_NP
+#define MB_NP 2
+#endif
+constexpr int kNP = MB_NP;
+constexpr int kSlots = 4, kSlotBytes = kNP * 8192, kGroups = 16;   // k-groups per layer
+constexpr int kDmaPerWave = kNP * 2;                               // 1 KiB DMAs per wave per group
 
 __device__ __forceinline__ float relu_i(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
@@ -58,7 +66,7 @@ __device__ __forceinline__ void dma(const Ring& r, int g, int k) {
 __device__ __forceinline__ void rd(const Ring& r, int lane, int slot, int t, Frag& f) {
     const char* s = r.lds + slot * kSlotBytes + lane * 16 + t * 1024;
     f.hi = *reinterpret_cast<const f16x8*>(s);
-    f.lo = *reinterpret_cast<const f16x8*>(s + 8192);
+    if constexpr (kNP == 2) f.lo = *reinterpret_cast<const f16x8*>(s + 8192);
 }
 
 template <int N>
@@ -70,6 +78,11 @@ __device__ __forceinline__ void enter() {
 
 __device__ __forceinline__ f32x4 mf16(const f16x8& a, const f16x8& b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mbf16(const f16x8& a, const f16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                   c, 0, 0, 0);
 }
 
 // split unit u (= 4 S + p) of the next k-step at tile t of half hf: NS = 2 the
@@ -89,7 +102,7 @@ __host__ __device__ constexpr int extra_stores() {
         const int u = unit_at<NS>(t, 0);
         if (u >= 0 && (u & 1)) { ++all; if (t < 7) ++before7; }
     }
-    return before7 + (kSlots - 2) * all;
+    return before7 + (kSlots - 2) * all;   // (kDmaPerWave DMAs per group counted by the caller)
 }
 
 template <int NS>
@@ -112,8 +125,8 @@ __device__ __forceinline__ void layer(const Ring& rg, int lane, Act<NS>& X, Act<
             for (int t = 0; t < 8; ++t) {
                 if (t + 1 < 8) rd(rg, lane, g % kSlots, t + 1, f[(t + 1) & 1]);
                 if (t == 7) {
-                    if constexpr (STORE) enter<4 * (kSlots - 2) + extra_stores<NS>()>();
-                    else enter<4 * (kSlots - 2)>();
+                    if constexpr (STORE) enter<kDmaPerWave * (kSlots - 2) + extra_stores<NS>()>();
+                    else enter<kDmaPerWave * (kSlots - 2)>();
                     rd(rg, lane, (g + 1) % kSlots, 0, f0);
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -121,11 +134,15 @@ __device__ __forceinline__ void layer(const Ring& rg, int lane, Act<NS>& X, Act<
 #pragma unroll
                 for (int S = 0; S < NS; ++S) {
                     f32x4 c = s == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : Y[8 * hf + t][S];
-                    c = mf16(w.lo, b[S].hi, c);
-                    c = mf16(w.hi, b[S].lo, c);
-                    Y[8 * hf + t][S] = mf16(w.hi, b[S].hi, c);
+                    if constexpr (kNP == 2) {
+                        c = mf16(w.lo, b[S].hi, c);
+                        c = mf16(w.hi, b[S].lo, c);
+                        Y[8 * hf + t][S] = mf16(w.hi, b[S].hi, c);
+                    } else {
+                        Y[8 * hf + t][S] = mbf16(w.hi, b[S].hi, c);
+                    }
                 }
-                if (t < 4) dma(rg, g + kSlots - 1, t);
+                if (t < kDmaPerWave) dma(rg, g + kSlots - 1, t);
                 const int u = unit_at<NS>(t, hf);
                 if (u >= 0) {
                     const int S = u >> 2, p = u & 3;
@@ -148,7 +165,7 @@ __device__ __forceinline__ void layer(const Ring& rg, int lane, Act<NS>& X, Act<
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < 3 * NS; ++i) {
+                for (int i = 0; i < (kNP == 2 ? 3 : 1) * NS; ++i) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                     __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
                 }
@@ -181,7 +198,7 @@ __global__ void __launch_bounds__(256, 1) mb_kernel(const char* __restrict__ w, 
 #pragma unroll
     for (int g = 0; g < kSlots - 1; ++g)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) dma(rg, g, k);
+        for (int k = 0; k < kDmaPerWave; ++k) dma(rg, g, k);
     const float seed = (float)(wv * 64 + lane) * 1e-4f;
     Frag f0;
     constexpr int kLayerFloats = NS * 4096;
@@ -241,14 +258,15 @@ void bench(const char* w, int pairs, float* save, float* out, uint64_t* stamps, 
     CK(hipEventElapsedTime(&ms, a, b));
     ms /= reps;
     const double samples = (double)blocks * 64 * NS, flop = samples * pairs * 2 * 2.0 * 256 * 256;
+    const double peak = kNP == 2 ? 8.389 : 25.166;   // fp32-equivalent ceiling (f16x3: 2517/3) / bf16 peak, x100 GF
     uint64_t* hs = (uint64_t*)malloc(blocks * 16);
     CK(hipMemcpy(hs, stamps, blocks * 16, hipMemcpyDeviceToHost));
     double cyc = 0, rt = 0;
     for (int i = 0; i < blocks; ++i) { cyc += hs[2 * i]; rt += hs[2 * i + 1]; }
     free(hs);
-    printf("samples/wave %d store %d: %.3f ms  %.1f TF fp32-equiv (%.1f%% of 839)  clock %.2f GHz  "
+    printf("np %d samples/wave %d store %d: %.3f ms  %.1f TF (%.1f%% of ceiling)  clock %.2f GHz  "
            "WG %.0f cyc (%.0f per 128 samples)\n",
-           16 * NS, STORE, ms, flop / ms / 1e9, flop / ms / 1e9 / 8.389, cyc / rt * 0.1, cyc / blocks,
+           kNP, 16 * NS, STORE, ms, flop / ms / 1e9, flop / ms / 1e9 / peak, cyc / rt * 0.1, cyc / blocks,
            cyc / blocks * 128.0 / (64 * NS));
     CK(hipEventDestroy(a));
     CK(hipEventDestroy(b));
