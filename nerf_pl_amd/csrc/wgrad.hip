@@ -313,7 +313,27 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
 #ifndef NR_W3_MULTI
 #define NR_W3_MULTI 1
 #endif
+// Cache policy of the saved-segment reads (each byte is read once).  The
+// bf16 LDS-DMA reads are non-temporal: fine-pass wgrad 1.447 -> 1.388 ms
+// (NR_W3_DMA_NT).  Non-temporal register loads in the f16x3 / bf16x6 staging
+// (NR_W3_NT=1) measured slower, 3.02 -> 3.13 ms (profiles/r02/nt_ab.txt).
+#ifndef NR_W3_NT
+#define NR_W3_NT 0
+#endif
+#ifndef NR_W3_DMA_NT
+#define NR_W3_DMA_NT 1
+#endif
 namespace w3 {
+template <class T>
+__device__ __forceinline__ T ld_seg(const T* p) {
+#if NR_W3_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+// cache policy bits of the bf16 segment DMA (2 = nt)
+constexpr int kDmaAux = NR_W3_DMA_NT ? 2 : 0;
 constexpr int kColB = 48;                        // bytes per column (16 pieces + pad)
 constexpr int kPlane = 256 * kColB;              // one piece of one operand
 constexpr int kOpnd = x3::kNP * kPlane;          // one operand (all pieces)
@@ -358,7 +378,7 @@ struct Stager {
     __device__ __forceinline__ void load(const float* base, int blk, int hb) {
         if constexpr (KIND == SEG_HEAD) {
             const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * 32 + 16 * hb + 2 * jp;
-            v0 = p[0]; v1 = p[1];
+            v0 = ld_seg(p); v1 = ld_seg(p + 1);
         } else {
             constexpr int F4 = Geo3<KIND, W>::CHUNKS * 64;
 #if NR_BF1      // bf16 segments (x3.h store_slot): 8-B slots, sample-major chunks, NR_SEGF block stride
@@ -368,7 +388,7 @@ struct Stager {
 #else
             const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * F4 +
                              Geo3<KIND, W>::f4(k, h, hb, 2 * jp);
-            v0 = p[0]; v1 = p[1];
+            v0 = ld_seg(p); v1 = ld_seg(p + 1);
 #endif
         }
     }
@@ -411,7 +431,7 @@ struct ThinStager {
 #if NR_BF1
         static_assert(KIND == SEG_HEAD, "bf16 runs no fused task pairs (kFuse)");
 #endif
-        v = *reinterpret_cast<const x3::f32x2*>(base + f);
+        v = ld_seg(reinterpret_cast<const x3::f32x2*>(base + f));
     }
     // split + store this thread's pair (times sc); s0/s1 += the unscaled values
     __device__ __forceinline__ void store(char* img, int nval, float& s0, float& s1, float sc) {
@@ -828,20 +848,20 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
         for (int i = wave; i < NDMA; i += 8) {
             if (i < TA) {
                 if (HEADA)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)img, 4, lane * 4, b * 256, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)img, 4, lane * 4, b * 256, 0, w3::kDmaAux);
                 else
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(img + i * kTile), 16, lane * 16,
-                                                             b * WA * 64 + i * 1024, 0, 0);
+                                                             b * WA * 64 + i * 1024, 0, w3::kDmaAux);
             } else if (i < TA + TB) {
                 const int t = i - TA;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(img + ABYTES + t * kTile), 16,
-                                                         lane * 16, b * WB * 64 + t * 1024, 0, 0);
+                                                         lane * 16, b * WB * 64 + t * 1024, 0, w3::kDmaAux);
             } else if constexpr (XMODE == 2) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr)(img + XOFF), 4, lane * 4, b * 256, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr)(img + XOFF), 4, lane * 4, b * 256, 0, w3::kDmaAux);
             } else if constexpr (XMODE == 1) {
                 const int t = i - TA - TB;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr)(img + XOFF + t * XTS), 16,
-                                                         lane * 16, b * XW * 64 + t * 1024, 0, 0);
+                                                         lane * 16, b * XW * 64 + t * 1024, 0, w3::kDmaAux);
             }
         }
     };

@@ -32,7 +32,7 @@ def main():
     p3, pb3 = ops.pack_fwd3(flat), ops.pack_bwd(flat, math="bf16x6")
     ph3, pbh3 = ops.pack_fwd3(flat, math="f16x3"), ops.pack_bwd(flat, math="f16x3")
     pb1, pbb1 = ops.pack_fwd3(flat, math="bf16"), ops.pack_bwd(flat, math="bf16")
-    n_rays, spr = 4096, 192
+    n_rays, spr = int(os.environ.get("NR_KB_RAYS", "4096")), 192   # NR_KB_RAYS: launch-size sweeps
     n = n_rays * spr
     rays = torch.randn(n_rays, 8, device=dev)
     rays[:, 3:6] = torch.nn.functional.normalize(rays[:, 3:6], dim=-1)
@@ -115,7 +115,7 @@ def main():
         tf = n * FLOP[k] / (ms * 1e-3) / 1e12
         extra = (f"  {tf / PEAKH3 * 100:5.1f}% of the f16x3 ceiling" if "h3" in k else
                  f"  {tf / PEAK3 * 100:5.1f}% of the bf16x6 ceiling" if "3" in k else "")
-        print(f"{k:8s} {ms:8.3f} ms  {tf:6.1f} TFLOP/s  {tf / 157.3 * 100:5.1f}% of fp32 MFMA peak"
+        print(f"{k:8s} n={n:8d} {ms:8.3f} ms  {tf:6.1f} TFLOP/s  {tf / 157.3 * 100:5.1f}% of fp32 MFMA peak"
               + extra, flush=True)
 
 
