@@ -527,7 +527,11 @@ def main():
     # fewer GPUs (NR_BENCH_DIST_BACKEND=gloo: RCCL refuses two ranks on one GPU)
     local %= max(1, torch.cuda.device_count())
     backend = os.environ.get("NR_BENCH_DIST_BACKEND", "nccl")
-    if world > 1:
+    # NR_BENCH_FORCE_DIST=1: the distributed path (process group, hook-launched
+    # gradient all-reduce, barriers, max-over-ranks timing) at one rank too --
+    # a real-RCCL rehearsal of the driver's N-GPU run on a one-GPU box
+    use_dist = world > 1 or os.environ.get("NR_BENCH_FORCE_DIST") == "1"
+    if use_dist:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -557,7 +561,7 @@ def main():
     if wl["train"]:
         params = [p for m in wl["models"] for p in m.parameters()]
         opt = FusedAdam(params, lr=5e-4, eps=1e-8)
-        if world > 1:
+        if use_dist:
             from nerf_pl_amd.distributed import GradAllReducer
             # one bucket per model: the fine model's all-reduce overlaps the
             # coarse model's backward
@@ -578,19 +582,19 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     timer.enabled = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     timer.enabled = False
-    if world > 1:
+    if use_dist:
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
@@ -669,7 +673,7 @@ def main():
             "final_loss": round(loss.item(), 5) if loss is not None else None,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

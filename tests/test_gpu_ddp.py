@@ -47,15 +47,21 @@ def _loss(models, emb, rays, draws, target, lo, hi):
     return torch.mean((res["rgb_coarse"] - t) ** 2) + torch.mean((res["rgb_fine"] - t) ** 2)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from nerf_pl_amd.distributed import GradAllReducer
         models, emb, rays, draws, target = _setup()
         params = [p for m in models for p in m.parameters()]
         red = GradAllReducer(params, buckets=[list(m.parameters()) for m in models])
+        dist.barrier()          # communicator set up on the main thread (bench.py does the same)
         per = N // world
         _loss(models, emb, rays, draws, target, rank * per, (rank + 1) * per).backward()
         red()
@@ -91,3 +97,34 @@ def test_two_rank_gradient_equals_single_process():
         for a, b in zip(grads, ref):
             scale = np.abs(b).max() + 1e-30
             assert np.abs(a - b).max() <= 1e-5 * scale, (rank, np.abs(a - b).max() / scale)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_rccl_one_rank_step_is_the_local_step():
+    """The RCCL (``nccl`` backend) path of the exchange on real hardware: one
+    rank, its gradient all-reduces (``ReduceOp.AVG``) launched from the
+    gradient hooks on autograd's thread, waited for before the optimizer
+    step.  Averaging over one rank is the identity, and the kernels are
+    deterministic, so the reduced gradient equals the local one bit for bit.
+    (RCCL refuses two ranks on one GPU; the two-rank exchange is
+    test_two_rank_gradient_equals_single_process, over gloo.)"""
+    models, emb, rays, draws, target = _setup()
+    _loss(models, emb, rays, draws, target, 0, N).backward()
+    ref = [p.grad.cpu().numpy() for m in models for p in m.parameters()]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    proc = ctx.Process(target=_worker, args=(0, 1, _free_port(), q, "nccl"))
+    proc.start()
+    rank, grads = q.get(timeout=100)
+    proc.join(timeout=60)
+    assert proc.exitcode == 0
+    assert len(grads) == len(ref)
+    for a, b in zip(grads, ref):
+        assert np.array_equal(a, b)
