@@ -341,6 +341,7 @@ def _models(dev):
 def wl_nerf_train(args, dev, rank, ndc):
     """cfg2 / cfg4 (Blender) and cfg3 (LLFF NDC) training steps."""
     from nerf_pl_amd import render_rays
+    from nerf_pl_amd.losses import MSELoss
     from nerf_pl_amd.rays import RaySampler, blender_focal, pose_spherical
     torch.manual_seed(1234 + rank)
     if ndc:
@@ -363,11 +364,12 @@ def wl_nerf_train(args, dev, rank, ndc):
     models, emb = _models(dev)
     torch.manual_seed(4321 + rank)            # per-rank seeds of the in-kernel Philox draws
     S, I = args.n_samples, args.n_importance
+    loss_fn = MSELoss()                       # losses.py:4-14 (train.py:107), one launch each way
 
     def step():
         rays, rgbs = sampler.next(args.batch)
         res = render_rays(models, emb, rays, S, False, 1.0, 1.0, I, 32768, False)
-        return torch.mean((res["rgb_coarse"] - rgbs) ** 2) + torch.mean((res["rgb_fine"] - rgbs) ** 2)
+        return loss_fn(res, rgbs)
 
     if ndc:
         name = "cfg3"
@@ -467,6 +469,7 @@ def shadow_scene(wh, n_poses, dev):
 def wl_shadow(args, dev, rank):
     """cfg5: train_efficient_sm.py:143-199 (sample_light_depth_every=1)."""
     from nerf_pl_amd import rendering_shadows as RS
+    from nerf_pl_amd.losses import MSELoss
     from nerf_pl_amd.rays import generate_rays
     wh, S, I, B = args.img, args.n_samples, args.n_importance, args.batch
     scene = shadow_scene(wh, args.poses, dev)
@@ -477,6 +480,7 @@ def wl_shadow(args, dev, rank):
     pos = [(rank * B) % total]
     tgt_pool = torch.rand(total, 3, device=dev)
     light_ppc = {"eye_pos": scene["light_eye"], "camera": scene["light_cam"]}
+    loss_fn = MSELoss()                       # train_efficient_sm.py's loss_dict['mse']
 
     def step():
         # dataset order (shuffle=False): B consecutive pixels of one view
@@ -495,11 +499,7 @@ def wl_shadow(args, dev, rank):
                                        32768, False, were_gradients_computed=False)
         out = RS.efficient_sm(scene["pixels"][sel % hw], scene["light_pixels"], cam, light, ppc,
                               light_ppc, (wh, wh), I > 0, I > 0, "shadow_method_2")
-        tgt = tgt_pool[sel]
-        loss = torch.mean((out["rgb_coarse"] - tgt) ** 2)
-        if "rgb_fine" in out:
-            loss = loss + torch.mean((out["rgb_fine"] - tgt) ** 2)
-        return loss
+        return loss_fn(out, tgt_pool[sel])
 
     return dict(name="cfg5",
                 metric=f"camera rays/sec shadow-mapping step ({S}c+{I}f, {wh}^2 light image "

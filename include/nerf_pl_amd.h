@@ -216,6 +216,20 @@ int nr_adam_step(float* const* params, const float* const* grads, float* const* 
                  double beta1, double beta2, double eps, double weight_decay, int64_t step,
                  void* stream);
 
+/* Training loss (losses.py:4-14 MSELoss: nn.MSELoss(reduction='mean') on
+ * rgb_coarse [+ on rgb_fine], the fine term added in fp32; metrics.py:4-13
+ * mse).  a, b (b may be NULL), target: n floats each.  loss (1 float, device);
+ * means (2 floats, device, may be NULL) = [mean (a-t)^2, mean (b-t)^2 (0
+ * without b)]; squares in fp32, sums in double in a fixed order
+ * (deterministic).  One launch. */
+int nr_mse_loss(const float* a, const float* b, const float* target, int64_t n, float* loss,
+                float* means, void* stream);
+/* Its backward: ga = (2/n) * (a - t) * g, gb likewise (torch's
+ * mse_loss_backward), g = the upstream gradient of the loss scalar (device
+ * pointer, 1 float); ga / gb may be NULL (not needed).  One launch. */
+int nr_mse_loss_bwd(const float* a, const float* b, const float* target, int64_t n,
+                    const float* g, float* ga, float* gb, void* stream);
+
 /* ---- shadow mapping (config 5: train_efficient_sm.py) ---------------------
  * get_normed_w column 3 (efficient_shadow_mapping.py:41-58): out (n) =
  * depth / (|camera @ pixel| + 1e-5); camera (3,3) row-major, pixels (n,3). */

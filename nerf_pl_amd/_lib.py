@@ -56,6 +56,8 @@ SIGNATURES = {
     "nr_adam_max_tensors": [],
     "nr_adam_step": [_p, _p, _p, _p, _p, _i, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                      ctypes.c_double, ctypes.c_double, _i64, _p],
+    "nr_mse_loss": [_p, _p, _p, _i64, _p, _p, _p],
+    "nr_mse_loss_bwd": [_p, _p, _p, _i64, _p, _p, _p, _p],
     "nr_sm_normed_depth": [_p, _p, _p, _i64, _p, _p],
     "nr_sm_forward": [_p, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _f, _f, _i, _f, _i64, _p, _p,
                       _p],

@@ -59,6 +59,10 @@ def _cases():
                          N, N], NR_EINVAL),
         ("nr_adam_step", [N, N, N, N, N, -1, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, N], NR_EINVAL),
         ("nr_adam_step", [N, N, N, N, N, 100000, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, N], NR_EINVAL),
+        ("nr_mse_loss", [N, N, N, 0, N, N, N], NR_EINVAL),      # the mean of nothing (torch: nan)
+        ("nr_mse_loss", [N, N, N, 5, N, N, N], NR_EINVAL),
+        ("nr_mse_loss_bwd", [N, N, N, -1, N, N, N, N], NR_EINVAL),
+        ("nr_mse_loss_bwd", [N, N, N, 5, N, N, N, N], NR_EINVAL),
         ("nr_sm_normed_depth", [N, N, N, -1, N, N], NR_EINVAL),
         ("nr_sm_backward", [N, N, 1, 1e-3, 1e-3, 0, -1, N, N], NR_EINVAL),
         ("nr_sm_forward", [N, N, N, N, 0, N, N, N, 128, 128, 2, 1e-3, 1e-3, 0, 1e-5, -1, N, N, N],
