@@ -268,7 +268,8 @@ __global__ void composite_bwd_kernel(CompBwdArgs a) {
 
 // ---------------------------------------------------------------------------
 // sample_pdf (rendering.py:14-48) + sort(cat[z_coarse, z_pdf]) (:257)
-// one wave per ray; cdf and merge staged in LDS
+// one wave per ray; cdf and merge staged in (dynamic) LDS:
+//   cdf [nb + 1] | coarse depths [S] | importance depths [P = pow2 >= I]
 // ---------------------------------------------------------------------------
 constexpr int kPdfMaxBins = 1024;
 constexpr int kMergeMax = 2048;
@@ -277,58 +278,104 @@ struct PdfArgs {
     const float* weights; int S;      // coarse weights (n_rays, S); bins = w[:, 1:S-1]
     const float* rays; const float* z_coarse;
     const float* u; const float* jitter; uint64_t seed;
-    int n_rays, I;
+    int n_rays, I, P;  // P: the importance region padded to a power of two
     float* z_pdf;      // (n_rays, I) or null
     float* z_fine;     // (n_rays, S + I) sorted, or null
 };
 
+// number of the n sorted values v[] that are < x (UPPER: <= x)
+template <bool UPPER>
+__device__ __forceinline__ int count_below(const float* v, int n, float x) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (UPPER ? v[mid] <= x : v[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
 __global__ void __launch_bounds__(64) sample_pdf_kernel(PdfArgs a) {
-    __shared__ float cdf[kPdfMaxBins + 1];
-    __shared__ float vals[kMergeMax];
+    extern __shared__ float pdf_lds[];
     const int lane = threadIdx.x;
     const int ray = blockIdx.x;
     if (ray >= a.n_rays) return;
     const int nb = a.S - 2;                     // N_samples_ - 2 bins
+    float* cdf = pdf_lds;
+    float* vals = pdf_lds + nb + 1;             // [coarse S | importance P]
     const float* w = a.weights + (size_t)ray * a.S + 1;
     for (int k = lane; k < nb; k += 64) cdf[k + 1] = w[k] + 1e-5f;   // :30
     __syncthreads();
+    // torch.sum (:31) then torch.cumsum (:32); CPU cumsum accumulates in
+    // double.  The two accumulations stay sequential (lane 0, the reference's
+    // order); the divisions by the sum run on every lane.
+    __shared__ float psum;
     if (lane == 0) {
-        // torch.sum (:31) then torch.cumsum (:32), CPU cumsum accumulates in double
         double tot = 0.0;
         for (int k = 0; k < nb; ++k) tot += (double)cdf[k + 1];
-        const float sum = (float)tot;
+        psum = (float)tot;
+    }
+    __syncthreads();
+    const float sum = psum;
+    for (int k = lane; k < nb; k += 64) cdf[k + 1] = cdf[k + 1] / sum;
+    __syncthreads();
+    if (lane == 0) {
         double run = 0.0;
         cdf[0] = 0.f;
         for (int k = 0; k < nb; ++k) {
-            run += (double)(cdf[k + 1] / sum);
+            run += (double)cdf[k + 1];
             cdf[k + 1] = (float)run;
         }
     }
     __syncthreads();
     const float near = a.rays[(size_t)ray * 8 + 6], far = a.rays[(size_t)ray * 8 + 7];
-    const int I = a.I, S = a.S, SF = S + I;
+    const int I = a.I, S = a.S, SF = S + I, P = a.P;
+    float* imp = vals + S;
     for (int j = lane; j < I; j += 64) {
         const int64_t idx = (int64_t)ray * I + j;
         const float u = a.u ? a.u[idx] : nr_rand_uniform(a.seed, 2, (uint64_t)idx);
         // searchsorted(cdf, u, side='right'): number of cdf entries <= u
-        int lo = 0, hi = nb + 1;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
-        }
-        float ind = (float)lo - 1.f;
+        float ind = (float)count_below<true>(cdf, nb + 1, u) - 1.f;
         ind = ind < 0.f ? 0.f : ind;                                    // :39
         const float jt = a.jitter ? a.jitter[idx] : nr_rand_uniform(a.seed, 3, (uint64_t)idx);
         const float t = nr_add(ind, jt) / (float)nb;                    // :41
         const float zs = nr_add(nr_mul(near, 1.f - t), nr_mul(far, t)); // :45
         if (a.z_pdf) a.z_pdf[idx] = zs;
-        vals[S + j] = zs;
+        imp[j] = zs;
     }
     if (!a.z_fine) return;
+    for (int j = I + lane; j < P; j += 64) imp[j] = __builtin_inff();
+    bool ok = true;
     for (int k = lane; k < S; k += 64) vals[k] = a.z_coarse[(size_t)ray * S + k];
     __syncthreads();
-    // rank sort (stable on ties, values only): position = #smaller + #equal-before
+    for (int k = lane; k + 1 < S; k += 64) ok &= vals[k] <= vals[k + 1];
     float* out = a.z_fine + (size_t)ray * SF;
+    // torch.sort of the values only: any sorting network gives the same
+    // output.  Coarse depths ascending (they are by construction, :216-232):
+    // bitonic sort of the importance depths, then a merge by binary searches
+    // (coarse first on ties).
+    if (__ballot(!ok) == 0) {
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = lane; i < P; i += 64) {
+                    const int ixj = i ^ j;
+                    if (ixj > i) {
+                        const float x = imp[i], y = imp[ixj];
+                        if ((x > y) == ((i & k) == 0)) { imp[i] = y; imp[ixj] = x; }
+                    }
+                }
+                __syncthreads();
+            }
+        for (int i = lane; i < S; i += 64) {
+            const float c = vals[i];
+            out[i + count_below<false>(imp, I, c)] = c;
+        }
+        for (int j = lane; j < I; j += 64) {
+            const float p = imp[j];
+            out[j + count_below<true>(vals, S, p)] = p;
+        }
+        return;
+    }
+    // otherwise a rank sort (stable on ties): position = #smaller + #equal-before
     for (int i = lane; i < SF; i += 64) {
         const float v = vals[i];
         int rank = 0;
@@ -421,9 +468,12 @@ NR_API int nr_sample_pdf(const float* weights, int n_samples, const float* rays,
     if (n_rays == 0 || n_importance == 0) return 0;
     NR_REQUIRE(weights && rays && (z_pdf || z_fine), "nr_sample_pdf: null pointer");
     NR_REQUIRE(!z_fine || z_coarse, "nr_sample_pdf: z_fine needs z_coarse");
-    PdfArgs a{weights, n_samples, rays, z_coarse, u, jitter, seed, (int)n_rays, n_importance,
+    int P = 1;
+    while (P < n_importance) P <<= 1;
+    PdfArgs a{weights, n_samples, rays, z_coarse, u, jitter, seed, (int)n_rays, n_importance, P,
               z_pdf, z_fine};
-    sample_pdf_kernel<<<(unsigned)n_rays, 64, 0, (hipStream_t)stream>>>(a);
+    const size_t lds = sizeof(float) * (size_t)(n_samples - 1 + n_samples + P);
+    sample_pdf_kernel<<<(unsigned)n_rays, 64, lds, (hipStream_t)stream>>>(a);
     NR_LAUNCH_CHECK("nr_sample_pdf");
     return 0;
 }
