@@ -333,7 +333,7 @@ __device__ __forceinline__ T ld_seg(const T* p) {
 #endif
 }
 // cache policy bits of the bf16 segment DMA (2 = nt)
-constexpr int kDmaAux = NR_W3_DMA_NT ? 2 : 0;
+[[maybe_unused]] constexpr int kDmaAux = NR_W3_DMA_NT ? 2 : 0;
 constexpr int kColB = 48;                        // bytes per column (16 pieces + pad)
 constexpr int kPlane = 256 * kColB;              // one piece of one operand
 constexpr int kOpnd = x3::kNP * kPlane;          // one operand (all pieces)
@@ -1112,20 +1112,32 @@ __device__ int wgrad_bias_dest(int t, int o) {
 }
 
 #if NR_F16
-// stats[l] = max over the per-wave maxima [l][nb] written by mlp_bwd3.hip
-__global__ void stats_reduce_kernel(float* __restrict__ stats, int nb) {
+// stats[l] = max over the per-wave maxima [l][nb] written by mlp_bwd3.hip;
+// 1024 threads per segment, four independent loads in flight per thread (the
+// max is order-independent: the result does not depend on the schedule)
+constexpr int kStatT = 1024;
+__global__ void __launch_bounds__(kStatT) stats_reduce_kernel(float* __restrict__ stats, int nb) {
     const int l = blockIdx.x;
     const float* w = stats + NR_STATS + (int64_t)l * nb;
-    float m = 0.f;
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) m = fmaxf(m, w[i]);
-    __shared__ float red[256];
-    red[threadIdx.x] = m;
-    __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
-        __syncthreads();
+    float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
+    int i = threadIdx.x;
+    for (; i + 3 * kStatT < nb; i += 4 * kStatT) {
+        m0 = fmaxf(m0, w[i]);
+        m1 = fmaxf(m1, w[i + kStatT]);
+        m2 = fmaxf(m2, w[i + 2 * kStatT]);
+        m3 = fmaxf(m3, w[i + 3 * kStatT]);
     }
-    if (threadIdx.x == 0) stats[l] = red[0];
+    for (; i < nb; i += kStatT) m0 = fmaxf(m0, w[i]);
+    float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) m = fmaxf(m, __shfl_xor(m, d));
+    __shared__ float red[kStatT / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kStatT / 64; ++k) m = fmaxf(m, red[k]);
+        stats[l] = m;
+    }
 }
 #endif
 
@@ -1273,7 +1285,7 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     a.x3 = x3;
     a.stats = NR_F16 ? SV + nr_sv_stats(nbp) : nullptr;
 #if NR_F16
-    stats_reduce_kernel<<<NR_STAT_SEGS, 256, 0, st>>>(SV + nr_sv_stats(nbp), (int)nbp);
+    stats_reduce_kernel<<<NR_STAT_SEGS, kStatT, 0, st>>>(SV + nr_sv_stats(nbp), (int)nbp);
     NR_LAUNCH_CHECK("nr_wgrad_stats");
     wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #elif NR_BF1
