@@ -18,7 +18,7 @@ flat = (torch.rand(packing.N_PARAMS, device=dev) - 0.5) * 0.15
 MATH = os.environ.get("NR_VAR_MATH", "f16x3")
 SFX, NP = {"f16x3": ("_h3", 2), "bf16": ("_b1", 1)}[MATH]
 ph, pbh = ops.pack_fwd3(flat, math=MATH), ops.pack_bwd(flat, math=MATH)
-n_rays, spr = 4096, 192
+n_rays, spr = int(os.environ.get("NR_VAR_RAYS", "4096")), 192
 n = n_rays * spr
 rays = torch.randn(n_rays, 8, device=dev)
 rays[:, 3:6] = torch.nn.functional.normalize(rays[:, 3:6], dim=-1)
