@@ -98,8 +98,12 @@ def _run(c, grad=False):
 CASES = list(range(24))
 
 
-@pytest.mark.parametrize("seed", CASES)
-def test_random_config_matches_oracle(seed):
+@pytest.mark.parametrize("seed,math", [(s, "f16x3") for s in CASES] +
+                         [(s, m) for s in CASES[:6] for m in ("bf16x6", "fp32")])
+def test_random_config_matches_oracle(seed, math, monkeypatch):
+    """every fp32-accurate MLP arithmetic meets the same bound"""
+    from nerf_pl_amd import ops
+    monkeypatch.setattr(ops, "MATH", math)
     c = _config(seed)
     _, _, res, ref, bad = _run(c)
     assert bad.sum() <= max(1, 0.02 * c["n"]), f"{bad.sum()} sample_pdf bin flips in {c}"
