@@ -81,3 +81,38 @@ def test_ray_sampler_epochs_are_permutations():
     assert torch.equal(torch.sort(ids).values, torch.arange(total))
     ref = RO.ray_buffer(poses, H, W, 10.0, 2.0, 6.0)[ids[-32:]]
     assert (rays.cpu() - ref).abs().max().item() < 2e-6
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_camera_rays_match_oracle(seed):
+    """Random image sizes (odd and even), focal lengths, pose sets and
+    near/far, Blender and NDC, against the restatement at the same bounds."""
+    from nerf_pl_amd.rays import generate_rays
+    r = np.random.default_rng(seed)
+    H, W = int(r.integers(1, 70)), int(r.integers(1, 70))
+    f = float(r.uniform(5.0, 200.0))
+    ndc = bool(seed % 2)
+    poses = []
+    for _ in range(int(r.integers(1, 4))):
+        if ndc:    # forward-facing: a small translation and a small rotation about z
+            a = float(r.uniform(-0.2, 0.2))
+            c2w = torch.tensor([[math.cos(a), -math.sin(a), 0.0, float(r.uniform(-0.2, 0.2))],
+                                [math.sin(a), math.cos(a), 0.0, float(r.uniform(-0.2, 0.2))],
+                                [0.0, 0.0, 1.0, float(r.uniform(-0.1, 0.1))]])
+        else:
+            from nerf_pl_amd.rays import pose_spherical
+            c2w = pose_spherical(float(r.uniform(-180, 180)), float(r.uniform(-80, 10)),
+                                 float(r.uniform(2.0, 6.0)))
+        poses.append(c2w)
+    poses = torch.stack(poses).float()
+    near, far = (0.0, 1.0) if ndc else (float(r.uniform(0.1, 2.0)), float(r.uniform(3.0, 200.0)))
+    ref = RO.ray_buffer(poses, H, W, f, near, far, ndc=ndc)
+    got = generate_rays(poses.to(DEV), H, W, f, near, far, ndc=ndc).cpu()
+    assert got.shape == ref.shape
+    if ndc:
+        rel = (got - ref).abs() / ref.abs().clamp_min(1.0)
+        assert rel.max().item() < 1e-5, (H, W, f)
+    else:
+        assert (got - ref).abs().max().item() < 2e-6, (H, W, f)
+        assert torch.equal(got[:, :3], ref[:, :3])
+    assert torch.equal(got[:, 6:], ref[:, 6:])
