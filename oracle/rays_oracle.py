@@ -6,8 +6,12 @@ Restates ``datasets/ray_utils.py`` in PyTorch-CPU fp32 with the reference's
 op order: ``get_ray_directions`` (:5-24; kornia's ``create_meshgrid`` with
 ``normalized_coordinates=False`` gives i = column, j = row, no +0.5),
 ``get_rays`` (:27-50) and ``get_ndc_rays`` (:53-93).  The reference module
-imports kornia, which is absent here, so it cannot be run: this restatement is
-the oracle ("parity unpinned" against the reference itself).
+imports kornia, which is absent here, so it cannot be imported whole; its
+kornia-free ``get_rays`` and ``get_ndc_rays`` are run as they stand by
+tests/golden/make_golden_rays.py, and tests/test_rays_golden.py pins this
+restatement to their outputs (bit-exact on the fixture host).
+``get_ray_directions`` (kornia's meshgrid) stays pinned only by that
+restatement of kornia 0.2.0's documented semantics.
 """
 from __future__ import annotations
 

@@ -116,3 +116,24 @@ def test_random_camera_rays_match_oracle(seed):
         assert (got - ref).abs().max().item() < 2e-6, (H, W, f)
         assert torch.equal(got[:, :3], ref[:, :3])
     assert torch.equal(got[:, 6:], ref[:, 6:])
+
+
+def test_rays_match_reference_fixtures():
+    """nr_gen_rays against the reference's own get_rays / get_ndc_rays outputs
+    (tests/golden/rays/rays.npz, tests/golden/make_golden_rays.py), same bounds."""
+    import os
+    from nerf_pl_amd.rays import generate_rays
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rays", "rays.npz"))
+    for k in range(int(z["n_cases"])):
+        H, W, f, ndc = z[f"c{k}_cfg"]
+        H, W, f, ndc = int(H), int(W), float(f), bool(ndc)
+        poses = torch.from_numpy(z[f"c{k}_poses"]).to(DEV)
+        got = generate_rays(poses, H, W, f, 0.0 if ndc else 2.0, 1.0 if ndc else 6.0,
+                            ndc=ndc).cpu().numpy()
+        exp = np.concatenate([z[f"c{k}_rays_o"], z[f"c{k}_rays_d"]], 1)
+        err = np.abs(got[:, :6] - exp)
+        if ndc:
+            assert (err / np.maximum(np.abs(exp), 1.0)).max() < 1e-5, k
+        else:
+            assert err.max() < 2e-6, k
+            assert np.array_equal(got[:, :3], exp[:, :3]), k
