@@ -12,6 +12,11 @@ parameter names (models/nerf.py:4-124), backed by the fused HIP kernels.
 * ``forward(x, sigma_only)`` accepts the pre-embedded input exactly like the
   reference (used e.g. by extract_color_mesh.py); ``render_rays`` takes the
   fused path that embeds in-kernel.
+* Any other configuration (``NeRF(D, W, in_xyz, in_dir, skips)``,
+  ``Embedding(C, F, logscale)``) is accepted too and runs composably on the
+  device: the reference's layer sequence on PyTorch-ROCm GEMMs, with
+  ``render_rays``'s sampling and compositing still on the HIP kernels
+  (SURVEY.md 8b).  Every caller of the reference uses the defaults.
 """
 from __future__ import annotations
 
@@ -22,23 +27,35 @@ from . import ops, packing
 
 
 class Embedding(nn.Module):
-    """x -> (x, sin(2^k x), cos(2^k x), ...), models/nerf.py:4-38 (logscale only)."""
+    """x -> (x, sin(f_0 x), cos(f_0 x), ...), models/nerf.py:4-38.  The
+    reference configuration (3 channels, log-scale bands) runs on nr_embed;
+    others compose the same sequence with torch ops on the device."""
 
     def __init__(self, in_channels, N_freqs, logscale=True):
         super().__init__()
-        if in_channels != 3 or not logscale:
-            raise NotImplementedError("nerf_pl_amd: only Embedding(3, F, logscale=True) "
-                                      "(the reference's configuration, train.py:34-35)")
         self.N_freqs = N_freqs
         self.in_channels = in_channels
+        self.logscale = logscale
         self.funcs = [torch.sin, torch.cos]
         self.out_channels = in_channels * (len(self.funcs) * N_freqs + 1)
-        self.freq_bands = 2 ** torch.linspace(0, N_freqs - 1, N_freqs)
+        if logscale:
+            self.freq_bands = 2 ** torch.linspace(0, N_freqs - 1, N_freqs)
+        else:
+            self.freq_bands = torch.linspace(1, 2 ** (N_freqs - 1), N_freqs)
+        self._fused = in_channels == 3 and logscale and N_freqs < 31
 
     def forward(self, x):
-        shp = x.shape
-        out = ops.embed(x.reshape(-1, 3), self.N_freqs)
-        return out.view(*shp[:-1], self.out_channels)
+        if not x.is_cuda:
+            raise ValueError("nerf_pl_amd.Embedding: input must be a HIP device tensor")
+        if self._fused:
+            shp = x.shape
+            out = ops.embed(x.reshape(-1, 3), self.N_freqs)
+            return out.view(*shp[:-1], self.out_channels)
+        out = [x]
+        for freq in self.freq_bands.tolist():
+            for func in self.funcs:
+                out += [func(freq * x)]
+        return torch.cat(out, -1)
 
 
 class NeRF(nn.Module):
@@ -46,9 +63,8 @@ class NeRF(nn.Module):
 
     def __init__(self, D=8, W=256, in_channels_xyz=63, in_channels_dir=27, skips=[4]):  # noqa: B006
         super().__init__()
-        if (D, W, in_channels_xyz, in_channels_dir, list(skips)) != (8, 256, 63, 27, [4]):
-            raise NotImplementedError("nerf_pl_amd: the fused kernels implement the reference "
-                                      "default NeRF(D=8, W=256, 63, 27, skips=[4])")
+        # the fused kernels implement the reference default; others compose
+        self._fused = (D, W, in_channels_xyz, in_channels_dir, list(skips)) == (8, 256, 63, 27, [4])
         self.D, self.W = D, W
         self.in_channels_xyz, self.in_channels_dir = in_channels_xyz, in_channels_dir
         self.skips = skips
@@ -75,6 +91,9 @@ class NeRF(nn.Module):
     def flat_params(self) -> torch.Tensor:
         """The flat fp32 buffer all parameters view into (re-flattened after
         ``.to()``/``load_state_dict`` replaced their storage)."""
+        if not self._fused:
+            raise RuntimeError("nerf_pl_amd.NeRF: flat/packed parameters exist for the fused "
+                               "default configuration only")
         ps = self.ordered_params()
         flat = self._flat
         ok = flat is not None and flat.device == ps[0].device
@@ -113,5 +132,29 @@ class NeRF(nn.Module):
         return c[1], c[2]
 
     def forward(self, x, sigma_only=False):
+        if not self._fused:
+            return self.forward_layers(x, sigma_only)
         from .functions import mlp_apply
         return mlp_apply(self, x=x, sigma_only=sigma_only)
+
+    def forward_layers(self, x, sigma_only=False):
+        """nerf.py:83-124 as a sequence of device GEMMs (configurations the fused
+        kernels do not implement)."""
+        if not x.is_cuda:
+            raise ValueError("nerf_pl_amd.NeRF: input must be a HIP device tensor")
+        if not sigma_only:
+            input_xyz, input_dir = torch.split(x, [self.in_channels_xyz, self.in_channels_dir], -1)
+        else:
+            input_xyz = x
+        xyz_ = input_xyz
+        for i in range(self.D):
+            if i in self.skips:
+                xyz_ = torch.cat([input_xyz, xyz_], -1)
+            xyz_ = getattr(self, f"xyz_encoding_{i + 1}")(xyz_)
+        sigma = self.sigma(xyz_)
+        if sigma_only:
+            return sigma
+        xyz_encoding_final = self.xyz_encoding_final(xyz_)
+        dir_encoding = self.dir_encoding(torch.cat([xyz_encoding_final, input_dir], -1))
+        rgb = self.rgb(dir_encoding)
+        return torch.cat([rgb, sigma], -1)

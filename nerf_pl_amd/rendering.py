@@ -9,8 +9,11 @@ Drop-in notes
 * ``chunk`` is accepted and ignored: the reference chunks the MLP only to bound
   memory (rendering.py:151-159); the fused kernel streams samples through
   registers and results do not depend on it.
-* ``embeddings`` must be the reference defaults (Embedding(3,10), Embedding(3,4));
-  the positional encoding is computed inside the fused MLP kernel.
+* with the reference defaults (Embedding(3,10), Embedding(3,4), NeRF()) the
+  positional encoding and the MLP run in the fused kernels; any other
+  embeddings or NeRF configuration takes the composable path (the reference's
+  ``inference`` sequence -- xyz, embeddings, model -- on device GEMMs), with
+  sampling and compositing on the same HIP kernels either way.
 * Everything runs on the HIP device that holds ``rays``; there is no CPU path.
 """
 from __future__ import annotations
@@ -25,14 +28,41 @@ from .rng import (STREAM_JITTER, STREAM_NOISE_COARSE, STREAM_NOISE_FINE, STREAM_
 __all__ = ["render_rays", "sample_pdf"]
 
 
-def _check_embeddings(embeddings):
+def _fused_ok(models, embeddings):
+    """True when the fused kernels implement this call: default NeRF models
+    and the reference's embeddings (train.py:34-35)."""
+    if any(m is not None and not getattr(m, "_fused", False) for m in models):
+        return False
     if embeddings is None:
-        return
-    e_xyz, e_dir = embeddings[0], embeddings[1]
-    for e, nf in ((e_xyz, 10), (e_dir, 4)):
-        if getattr(e, "N_freqs", nf) != nf or getattr(e, "in_channels", 3) != 3:
-            raise NotImplementedError("nerf_pl_amd.render_rays: embeddings must be "
-                                      "[Embedding(3, 10), Embedding(3, 4)] (train.py:34-35)")
+        return True
+    for e, nf in ((embeddings[0], 10), (embeddings[1], 4)):
+        if (getattr(e, "N_freqs", None) != nf or getattr(e, "in_channels", None) != 3
+                or not getattr(e, "logscale", True)):
+            return False
+    return True
+
+
+def _check_embeddings(embeddings, models=()):
+    """The shadow-mapping path (rendering_shadows) runs the fused kernels only."""
+    if not _fused_ok(models, embeddings):
+        raise NotImplementedError("nerf_pl_amd.rendering_shadows: the default NeRF() and "
+                                  "[Embedding(3, 10), Embedding(3, 4)] only (train_efficient_sm.py:45-56)")
+
+
+def _composable_mlp(model, embeddings, rays, z, spr, sigma_only=False):
+    """rendering.py:141-161 for a configuration the fused kernels do not
+    implement: xyz = o + d z (:234, multiply then add), the embeddings, and the
+    model on the embedded input (dir embedding repeated per sample, :145)."""
+    if embeddings is None:
+        raise ValueError("nerf_pl_amd.render_rays: a non-default NeRF needs its embeddings")
+    n = rays.shape[0]
+    dz = rays[:, None, 3:6] * z.reshape(n, spr)[:, :, None]
+    xyz = (rays[:, None, 0:3] + dz).reshape(-1, 3)
+    e = embeddings[0](xyz)
+    if sigma_only:
+        return model(e, sigma_only=True)
+    d = torch.repeat_interleave(embeddings[1](rays[:, 3:6]), repeats=spr, dim=0)
+    return model(torch.cat([e, d], 1))
 
 
 def sample_pdf(rays, weights, N_importance, det=False, eps=1e-5, *, rng=None):
@@ -58,7 +88,13 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
                 N_importance=0, chunk=1024 * 32, white_back=False, test_time=False, *, rng=None,
                 _capture=None):
     del chunk
-    _check_embeddings(embeddings)
+    fused = _fused_ok(models, embeddings)
+
+    def mlp(model, z, spr, sigma_only=False):
+        if fused:
+            return mlp_apply(model, rays=rays, z=z, spr=spr, sigma_only=sigma_only)
+        return _composable_mlp(model, embeddings, rays, z, spr, sigma_only)
+
     rays = ops._dev(rays, "rays", 8)
     dev = rays.device
     n_rays = rays.shape[0]
@@ -81,13 +117,13 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
     if test_time:
         # sigma-only coarse pass, weights only (rendering.py:237-241)
         with torch.no_grad():
-            sig = mlp_apply(models[0], rays=rays, z=z_c, spr=N_samples, sigma_only=True)
+            sig = mlp(models[0], z_c, N_samples, sigma_only=True)
             _, _, opac_c, w_c = ops.composite_forward(sig, z_c, rays, noise_c, noise_std, seed,
                                                       STREAM_NOISE_COARSE, white_back,
                                                       weights_only=True)
         result["opacity_coarse"] = opac_c
     else:
-        raw_c = mlp_apply(models[0], rays=rays, z=z_c, spr=N_samples)
+        raw_c = mlp(models[0], z_c, N_samples)
         rgb_c, depth_c, opac_c, w_c = composite_apply(raw_c, z_c, rays, noise_c, noise_std, seed,
                                                       STREAM_NOISE_COARSE, white_back)
         result["rgb_coarse"] = rgb_c
@@ -104,7 +140,7 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
         cap["z_fine"] = z_f
         s_f = N_samples + N_importance
         noise_f = rng.randn((n_rays, s_f), dev)
-        raw_f = mlp_apply(models[1], rays=rays, z=z_f, spr=s_f)
+        raw_f = mlp(models[1], z_f, s_f)
         rgb_f, depth_f, opac_f, _ = composite_apply(raw_f, z_f, rays, noise_f, noise_std, seed,
                                                     STREAM_NOISE_FINE, white_back)
         result["rgb_fine"] = rgb_f

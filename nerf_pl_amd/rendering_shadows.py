@@ -39,7 +39,7 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
                 N_importance=0, chunk=1024 * 32, white_back=False, test_time=False,
                 were_gradients_computed=True, *, rng=None):
     del chunk, white_back, were_gradients_computed
-    _check_embeddings(embeddings)
+    _check_embeddings(embeddings, models)
     rays = ops._dev(rays, "rays", 8)
     dev = rays.device
     n_rays = rays.shape[0]

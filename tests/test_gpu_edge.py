@@ -201,7 +201,7 @@ def test_bad_inputs_raise():
         render_rays(models, _emb(), rays[:, :7], 8, False, 0, 1, 0)
     with pytest.raises(TypeError):               # float32 only
         render_rays(models, _emb(), rays.double(), 8, False, 0, 1, 0)
-    with pytest.raises(NotImplementedError):     # non-default embeddings
+    with pytest.raises((RuntimeError, ValueError)):   # embedding width != the model's input
         render_rays(models, [Embedding(3, 8), Embedding(3, 4)], rays, 8, False, 0, 1, 0)
     with pytest.raises(ValueError):              # replayed draw of the wrong shape
         render_rays(models, _emb(), rays, 8, False, 1.0, 1, 0,
