@@ -95,8 +95,13 @@ def kernel_roofline(k, events, math_, traffic_json):
         tsrc = f"{t.get('file', 'profiles/r01/traffic.json')} ({t['method']})"
     common = dict(kernel=k, traffic=traffic, traffic_unit="GB per launch", traffic_source=tsrc,
                   samples_per_launch=nmax, avg_launch_ms=round(avg, 4))
-    if k == "mlp_wgrad":
-        bps = BYTES_WGRAD_BF16 if math_ == "bf16" else BYTES_WGRAD
+    np_ = SPLIT_PRODUCTS.get(math_)
+    peak = BF16_MFMA_PEAK_TF / np_ if np_ else FP32_MFMA_PEAK_TF
+    # the weight gradient streams every saved segment once at 60 FLOP/B: below
+    # the ridge (peak FLOP/s / 8 TB/s) of the split arithmetics, HBM-bound;
+    # above the fp32 MFMA ridge (19.7 FLOP/B), MFMA-bound
+    bps = BYTES_WGRAD_BF16 if math_ == "bf16" else BYTES_WGRAD
+    if k == "mlp_wgrad" and flops / bps < peak * 1e12 / (HBM_PEAK_GBS * 1e9):
         ach = bps * nmax / (avg * 1e-3) / 1e9
         return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 4), bytes_per_sample=bps,
@@ -104,8 +109,6 @@ def kernel_roofline(k, events, math_, traffic_json):
                                 "(2436 values/sample) segment read once, "
                                 + ("bf16" if math_ == "bf16" else "fp32"),
                     tflops_fp32_equiv=round(tflops, 2), **common)
-    np_ = SPLIT_PRODUCTS.get(math_)
-    peak = BF16_MFMA_PEAK_TF / np_ if np_ else FP32_MFMA_PEAK_TF
     basis = {
         "bf16x6": "bf16x6: fp32 FLOPs on v_mfma_f32_16x16x32_bf16, six bf16 products per "
                   f"fp32 product -> ceiling = dense bf16 peak {BF16_MFMA_PEAK_TF:.0f} / 6",
@@ -116,7 +119,8 @@ def kernel_roofline(k, events, math_, traffic_json):
     }.get(math_, "fp32: v_mfma_f32_32x32x2_f32 dense peak")
     return dict(bound="mfma", achieved=round(tflops, 2), peak=round(peak, 1), unit="TFLOP/s",
                 frac=round(tflops / peak, 4), flop_per_sample=flops, peak_basis=basis,
-                frac_of_fp32_mfma_peak=round(tflops / FP32_MFMA_PEAK_TF, 4), **common)
+                **{("frac_of_fp32_mfma_peak" if math_ == "fp32" else "speed_vs_fp32_mfma_peak"):
+                   round(tflops / FP32_MFMA_PEAK_TF, 4)}, **common)
 
 
 def _math():
@@ -142,6 +146,18 @@ def parse():
     ap.add_argument("--light-shard", action="store_true",
                     help="cfg5 with N>1: render the light image sharded over the ranks and "
                          "all-gather the maps (SURVEY 8e phase 2) instead of on every rank")
+    ap.add_argument("--grad-on-light", action="store_true",
+                    help="cfg5: train_efficient_sm.py --grad_on_light (the mode 60 of the "
+                         "reference's 63 launchers use): the light image rendered under "
+                         "autograd every step, the shadow loss back-propagated into it")
+    ap.add_argument("--light-importance", type=int, default=None,
+                    help="cfg5: Light_N_importance (default 64; -1 = a random choice of "
+                         "{0, 8, 16, 32} per step, train_efficient_sm.py:153-154, drawn from a "
+                         "generator seeded alike on every rank)")
+    ap.add_argument("--fp32-leg-steps", type=int, default=5,
+                    help="after the timed region, time this many steps with the exact fp32 "
+                         "MLP arithmetic (v_mfma_f32_32x32x2_f32) for the fp32-MFMA roofline; "
+                         "0 disables")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="weak: --batch rays per rank (the driver's default); strong: --batch "
                          "rays per step in total, split over the ranks (SURVEY 8e)")
@@ -157,6 +173,8 @@ def parse():
     a.img = a.img or d[1]
     a.n_samples = a.n_samples or d[2]
     a.n_importance = a.n_importance if a.n_importance is not None else d[3]
+    if a.light_importance is None:
+        a.light_importance = a.n_importance
     return a
 
 
@@ -343,7 +361,6 @@ def wl_nerf_train(args, dev, rank, ndc):
     from nerf_pl_amd import render_rays
     from nerf_pl_amd.losses import MSELoss
     from nerf_pl_amd.rays import RaySampler, blender_focal, pose_spherical
-    torch.manual_seed(1234 + rank)
     if ndc:
         W, H, focal, near, far = 504, 378, 407.0, 0.0, 1.0
         poses = []
@@ -358,9 +375,13 @@ def wl_nerf_train(args, dev, rank, ndc):
         focal, near, far = blender_focal(W), 1.0, 200.0   # datasets/blender.py:40-41
         poses = torch.stack([pose_spherical(-180.0 + 360.0 * k / args.poses, -30.0, 4.0)
                              for k in range(args.poses)]).to(dev)
+    torch.manual_seed(1234)                   # the same target colours on every rank
     pool_rgb = torch.rand(poses.shape[0] * H * W, 3, device=dev)
+    # one permutation per epoch shared by the ranks, rank r taking perm[r::world]
+    # (DistributedSampler under Lightning DDP, train.py:89-94)
+    world = dist.get_world_size() if dist.is_initialized() else 1
     sampler = RaySampler(poses, H, W, focal, near, far, rgb_pool=pool_rgb, ndc=ndc,
-                         seed=99 + rank)
+                         seed=99, rank=rank, world=world)
     models, emb = _models(dev)
     torch.manual_seed(4321 + rank)            # per-rank seeds of the in-kernel Philox draws
     S, I = args.n_samples, args.n_importance
@@ -467,11 +488,13 @@ def shadow_scene(wh, n_poses, dev):
 
 
 def wl_shadow(args, dev, rank):
-    """cfg5: train_efficient_sm.py:143-199 (sample_light_depth_every=1)."""
+    """cfg5: train_efficient_sm.py:139-208 (sample_light_depth_every=1)."""
+    import numpy as np
     from nerf_pl_amd import rendering_shadows as RS
     from nerf_pl_amd.losses import MSELoss
     from nerf_pl_amd.rays import generate_rays
     wh, S, I, B = args.img, args.n_samples, args.n_importance, args.batch
+    LI = args.light_importance
     scene = shadow_scene(wh, args.poses, dev)
     models, emb = _models(dev)
     torch.manual_seed(4321 + rank)
@@ -481,6 +504,11 @@ def wl_shadow(args, dev, rank):
     tgt_pool = torch.rand(total, 3, device=dev)
     light_ppc = {"eye_pos": scene["light_eye"], "camera": scene["light_cam"]}
     loss_fn = MSELoss()                       # train_efficient_sm.py's loss_dict['mse']
+    # Light_N_importance == -1: np.random.choice([0, 8, 16, 32]) per light render
+    # (:153-154); one generator seeded alike on every rank keeps the ranks'
+    # light renders the same shape (the sharded render gathers them)
+    li_rng = np.random.RandomState(2024)
+    shard = args.light_shard and dist.is_initialized() and dist.get_world_size() > 1
 
     def step():
         # dataset order (shuffle=False): B consecutive pixels of one view
@@ -490,31 +518,40 @@ def wl_shadow(args, dev, rank):
         pose = sel // hw
         ppc = {"eye_pos": scene["eyes"][pose], "camera": scene["mats"][pose]}
         cam = RS.render_rays(models, emb, rays, S, False, 1.0, 0.0, I, 32768, False)
-        if args.light_shard and dist.is_initialized() and dist.get_world_size() > 1:
-            light = RS.render_rays_sharded(models, emb, scene["light_rays"], S, False, 1.0, 0.0, I,
-                                           32768, False)
-        else:
-            with torch.no_grad():
-                light = RS.render_rays(models, emb, scene["light_rays"], S, False, 1.0, 0.0, I,
+        li = int(li_rng.choice([0, 8, 16, 32])) if LI == -1 else LI
+        # --grad_on_light renders the light under autograd (:158-162), else no_grad (:164-168)
+        with torch.set_grad_enabled(args.grad_on_light):
+            if shard:
+                light = RS.render_rays_sharded(models, emb, scene["light_rays"], S, False, 1.0,
+                                               0.0, li, 32768, False)
+            else:
+                light = RS.render_rays(models, emb, scene["light_rays"], S, False, 1.0, 0.0, li,
                                        32768, False, were_gradients_computed=False)
         out = RS.efficient_sm(scene["pixels"][sel % hw], scene["light_pixels"], cam, light, ppc,
-                              light_ppc, (wh, wh), I > 0, I > 0, "shadow_method_2")
+                              light_ppc, (wh, wh), I > 0, li > 0, "shadow_method_2")
         return loss_fn(out, tgt_pool[sel])
 
+    lname = "random {0,8,16,32}" if LI == -1 else str(LI)
+    # light samples per light ray: coarse S, plus S + li fine when li > 0
+    lis = [0, 8, 16, 32] if LI == -1 else [LI]
+    light_samples = S + sum((S + li) if li > 0 else 0 for li in lis) / len(lis)
+    gol = args.grad_on_light
     return dict(name="cfg5",
                 metric=f"camera rays/sec shadow-mapping step ({S}c+{I}f, {wh}^2 light image "
-                       "re-rendered per step)",
+                       f"re-rendered per step{', --grad_on_light' if gol else ''})",
                 workload=f"cfg5: train_efficient_sm.py step at {wh}x{wh}: sigma-only render of "
-                         f"{B} camera rays/rank ({S}+{I}, noise_std=0, with gradients) + no_grad "
-                         f"render of the {hw}-ray light image ({S}+{I}"
+                         f"{B} camera rays/rank ({S}+{I}, noise_std=0, with gradients) + "
+                         f"{'autograd' if gol else 'no_grad'} render of the {hw}-ray light image "
+                         f"({S}+{lname}"
                          f"{', sharded over the ranks + all-gather' if args.light_shard else ''}) + efficient_sm "
-                         "(shadow_method_2, per-pose runs) + MSE + backward + Adam lr 5e-4",
+                         "(shadow_method_2, per-pose runs) + MSE + backward"
+                         f"{' (through the light render too)' if gol else ''} + Adam lr 5e-4",
                 data=f"synthetic ({args.poses}-pose camera orbit + one light camera, rays "
                      "generated on device, random targets, seeded default-init NeRF pair)",
                 step=step, train=True, models=models, rays_per_step=B,
                 samples_per_ray=S + I,
                 flop_per_ray=(S + (S + I)) * FLOP_TRAIN_SIGMA
-                + hw / B * (S * FLOP_FWD_SIGMA + (S + I) * FLOP_FWD_SIGMA),
+                + hw / B * light_samples * (FLOP_TRAIN_SIGMA if gol else FLOP_FWD_SIGMA),
                 cpu=lambda budget: cpu_shadow(args, budget, scene))
 
 
@@ -580,44 +617,89 @@ def main():
             opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    timer.enabled = True
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    timer.enabled = False
-    if use_dist:
-        t = torch.tensor([el], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = t.item()
+    def run(steps, warmup):
+        """warmup untimed steps, then `steps` timed ones between barriers;
+        (seconds = max over ranks, last loss)."""
+        loss = None
+        for _ in range(warmup):
+            step()
+        if use_dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        timer.events = {}
+        timer.enabled = True
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = step()
+        if use_dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        timer.enabled = False
+        if use_dist:
+            t = torch.tensor([el], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+        return el, loss
+
+    def rooflines(math_, ms, steps):
+        fp32_key = "frac_of_fp32_mfma_peak" if math_ == "fp32" else "speed_vs_fp32_mfma_peak"
+        ks = timer.summary()
+        roof, roofs, stage = None, {}, None
+        if ks:
+            tj = {}
+            for rel in ("profiles/r03/traffic.json", "profiles/r02/traffic.json",
+                        "profiles/r01/traffic.json"):
+                tf = os.path.join(REPO, rel)
+                if os.path.exists(tf):
+                    tj = {k: dict(v, file=rel) for k, v in json.load(open(tf)).items()
+                          if isinstance(v, dict)}
+                    break
+            for k in KERNEL_FLOP:
+                if k in ks:
+                    roofs[k] = kernel_roofline(k, timer.events[k], math_, tj)
+            if roofs:
+                dom = max(roofs, key=lambda k: ks[k]["total_ms"])
+                roof = roofs[dom]
+                ks[dom]["share_of_step"] = ks[dom]["total_ms"] / (ms * steps)
+                # the MLP stage (every fused MLP launch: forward, data and weight
+                # gradients) against the fp32 MFMA peak -- the north star's ratio
+                fl = sum(KERNEL_FLOP[k] * n for k in roofs for *_, n in timer.events[k])
+                t = sum(ks[k]["total_ms"] for k in roofs)
+                tf_ = fl / (t * 1e-3) / 1e12
+                stage = dict(kernels=sorted(roofs), ms_per_step=round(t / steps, 4),
+                             share_of_step=round(t / (ms * steps), 4),
+                             tflops_fp32_equiv=round(tf_, 2),
+                             fp32_mfma_peak=FP32_MFMA_PEAK_TF,
+                             **{fp32_key: round(tf_ / FP32_MFMA_PEAK_TF, 4)})
+        return ks, roof, roofs, stage
+
+    el, loss = run(args.steps, args.warmup)
     ms = el / args.steps * 1e3
     rays_per_s = wl["rays_per_step"] * world * args.steps / el
+    math_main = _math()
+    ks, roof, roofs, stage = rooflines(math_main, ms, args.steps)
 
-    ks = timer.summary()
-    roof, roofs = None, {}
-    if ks:
-        math_ = _math()
-        tj = {}
-        for rel in ("profiles/r02/traffic.json", "profiles/r01/traffic.json"):
-            tf = os.path.join(REPO, rel)
-            if os.path.exists(tf):
-                tj = {k: dict(v, file=rel) for k, v in json.load(open(tf)).items()
-                      if isinstance(v, dict)}
-                break
-        for k in KERNEL_FLOP:
-            if k in ks:
-                roofs[k] = kernel_roofline(k, timer.events[k], math_, tj)
-        dom = max(roofs, key=lambda k: ks[k]["total_ms"])
-        roof = roofs[dom]
-        ks[dom]["share_of_step"] = ks[dom]["total_ms"] / (ms * args.steps)
+    # exact-fp32 leg: the same workload on v_mfma_f32_32x32x2_f32 (fp32
+    # products, no operand splitting) -- its own roofline against the fp32
+    # MFMA peak, next to the default arithmetic's
+    fp32_leg = None
+    if args.fp32_leg_steps > 0 and math_main != "fp32":
+        from nerf_pl_amd import ops as _ops
+        _ops.MATH = "fp32"
+        try:
+            el32, _ = run(args.fp32_leg_steps, 2)
+        finally:
+            _ops.MATH = math_main
+        ms32 = el32 / args.fp32_leg_steps * 1e3
+        ks32, roof32, roofs32, stage32 = rooflines("fp32", ms32, args.fp32_leg_steps)
+        fp32_leg = dict(dtype="fp32", mlp_arithmetic="fp32 (v_mfma_f32_32x32x2_f32: exact fp32 "
+                        "products, fp32 accumulation)", steps=args.fp32_leg_steps, warmup=2,
+                        value=round(wl["rays_per_step"] * world * args.fp32_leg_steps / el32, 1),
+                        unit="rays/s", ms_per_step=round(ms32, 3), roofline=roof32,
+                        rooflines=roofs32, mlp_stage=stage32,
+                        kernels={k: {kk: round(vv, 4) if isinstance(vv, float) else vv
+                                     for kk, vv in v.items()} for k, v in ks32.items()})
 
     cpu = None
     cpu1 = None
@@ -644,7 +726,9 @@ def main():
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
-            "dtype": "bf16" if _math() == "bf16" else "fp32",
+            # the arithmetic the MLP computes in: f16x3 = fp32 operands
+            # split into two fp16 pieces on fp16 matrix cores (not plain fp32)
+            "dtype": math_main,
             "mlp_arithmetic": {
                 "bf16x6": "bf16x6 (fp32 operands split exactly into 3 bf16 pieces, 6 piece "
                           "products accumulated in fp32; fp32-level accuracy, parity-tested "
@@ -666,6 +750,8 @@ def main():
             "model_tflops": round(rays_per_s * wl["flop_per_ray"] / 1e12, 2),
             "roofline": roof,
             "rooflines": roofs,
+            "mlp_stage": stage,
+            "fp32_leg": fp32_leg,
             "cpu_baseline": cpu,
             "cpu_baseline_1thread": cpu1,
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv

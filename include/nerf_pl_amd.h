@@ -230,11 +230,45 @@ int nr_mse_loss(const float* a, const float* b, const float* target, int64_t n, 
 int nr_mse_loss_bwd(const float* a, const float* b, const float* target, int64_t n,
                     const float* g, float* ga, float* gb, void* stream);
 
+/* losses.py:28-73 OpactiyLoss (loss_dict['opacity']; train_efficient_sm.py:43
+ * constructs it, :191 evaluates it on the light render): with gray = (t0 + t1 +
+ * t2) / 3 of target rows t (n_t,3), sm = gray > thres, non = !sm,
+ *   loss = coeff - |mean(o_c[non]) - mean(o_c[sm])| [+ the same on o_f],
+ * 0 when either set is empty.  The targets index rows 0..n_t-1 of the n_o
+ * opacities (n_t <= n_o).  loss: 1 float; stats: 8 floats kept for the
+ * backward.  One launch, fixed-order double sums (deterministic). */
+int nr_opacity_loss(const float* opacity_c, const float* opacity_f, const float* target,
+                    int64_t n_t, int64_t n_o, float thres, float coeff, float* loss, float* stats,
+                    void* stream);
+/* Its backward: g (device, 1 float) -> g_opacity_c / g_opacity_f (n_o each,
+ * either may be NULL); rows >= n_t get 0.  One launch. */
+int nr_opacity_loss_bwd(const float* target, int64_t n_t, int64_t n_o, float thres,
+                        const float* stats, const float* g, float* g_opacity_c,
+                        float* g_opacity_f, void* stream);
+
+/* torchsearchsorted.searchsorted(a, v, out, side) -- the reference's only
+ * native dependency (.gitmodules:1-3; rendering.py:2,37, rendering_rgb_sm.py:2,40)
+ * as a standalone call (nr_sample_pdf fuses it on the render path): out
+ * (nrows, ncols_v) int64 = per row the number of entries of the sorted row of a
+ * that are < v (side_right = 0) or <= v (side_right = 1).  nrows_a == nrows_v,
+ * or either is 1 (shared by every row).  torch.searchsorted's comparisons (a
+ * NaN query lands after every entry).  float32 and float64 variants. */
+int nr_searchsorted(const float* a, const float* v, int64_t nrows_a, int64_t ncols_a,
+                    int64_t nrows_v, int64_t ncols_v, int side_right, int64_t* out, void* stream);
+int nr_searchsorted_f64(const double* a, const double* v, int64_t nrows_a, int64_t ncols_a,
+                        int64_t nrows_v, int64_t ncols_v, int side_right, int64_t* out,
+                        void* stream);
+
 /* ---- shadow mapping (config 5: train_efficient_sm.py) ---------------------
- * get_normed_w column 3 (efficient_shadow_mapping.py:41-58): out (n) =
+ * get_normed_w column 3 (efficient_shadow_mapping.py:47-62): out (n) =
  * depth / (|camera @ pixel| + 1e-5); camera (3,3) row-major, pixels (n,3). */
 int nr_sm_normed_depth(const float* camera, const float* pixels, const float* depth, int64_t n,
                        float* out, void* stream);
+/* Its autograd (:59, `pixel_depth[:,3] / norm`): g_depth (n) = g_out / (|camera @ pixel| +
+ * 1e-5).  The light render's path to its depths when the light map is trained
+ * (train_efficient_sm.py --grad_on_light, :158-162). */
+int nr_sm_normed_depth_bwd(const float* camera, const float* pixels, const float* g_out,
+                           int64_t n, float* g_depth, void* stream);
 
 /* efficient_sm's shadow maps (rendering_shadows.py:359-482 with
  * efficient_shadow_mapping.py:19-130): for camera rays with pixels (n,3) and
@@ -244,18 +278,25 @@ int nr_sm_normed_depth(const float* camera, const float* pixels, const float* de
  * camera (3,3) + eye (3) and the light's normed depth map light_w (res_w*res_h)
  * -> out (n,3) = shadow value + out_eps.  method 1: clip(max(d/delta, epsilon));
  * method 2: per-run min-max normalisation (+ sigmoid).  workspace:
- * nr_sm_workspace_bytes(n); keep it for nr_sm_backward. */
-int64_t nr_sm_workspace_bytes(int64_t n);
+ * nr_sm_workspace_bytes(n, res_w*res_h) bytes; keep it for nr_sm_backward. */
+int64_t nr_sm_workspace_bytes(int64_t n, int64_t n_light);
 int nr_sm_forward(const float* pixels, const float* depth, const float* eye, const float* cameras,
                   int per_ray, const float* light_camera, const float* light_eye,
                   const float* light_w, int res_w, int res_h, int method, float delta,
                   float epsilon, int sigmoid, float out_eps, int64_t n, void* workspace,
                   float* out, void* stream);
-/* Autograd of nr_sm_forward w.r.t. the camera depth: g_out (n,3) -> g_depth (n).
- * The light map is treated as a constant (train_efficient_sm.py renders it
- * under no_grad unless --grad_on_light). */
+/* Autograd of nr_sm_forward: g_out (n,3) -> g_depth (n), the camera depths,
+ * and g_light_w (n_light = res_w*res_h), the light's normed depth map (the
+ * backward of the texel gather w_light.view(w,h)[v,u], :98, including the
+ * min-max normalisation's dependence on each run's extremes, :10-11,122).
+ * Either output may be NULL (not needed; train_efficient_sm.py renders the
+ * light under no_grad unless --grad_on_light).  The light-map gradient is a
+ * deterministic scatter-add (64-bit fixed point at one power-of-two scale per
+ * call, integer atomics: bitwise reproducible, exact to ~2^-60 of the largest
+ * contribution); untouched texels get 0. */
 int nr_sm_backward(const float* g_out, void* workspace, int method, float delta, float epsilon,
-                   int sigmoid, int64_t n, float* g_depth, void* stream);
+                   int sigmoid, int64_t n, int64_t n_light, float* g_depth, float* g_light_w,
+                   void* stream);
 
 /* Test hook: one v_mfma_f32_32x32x2_f32 on A (32x2), B (2x32) -> D (32x32). */
 int nr_probe_mfma32(const float* a, const float* b, float* d, void* stream);

@@ -6,6 +6,8 @@ render_rays / sample_pdf / NeRF hot path.
 from .nerf import Embedding, NeRF
 from .rendering import render_rays, sample_pdf
 from .rng import PhiloxRNG, ReplayRNG
+from .searchsorted import searchsorted
 
-__all__ = ["Embedding", "NeRF", "render_rays", "sample_pdf", "PhiloxRNG", "ReplayRNG"]
+__all__ = ["Embedding", "NeRF", "render_rays", "sample_pdf", "searchsorted", "PhiloxRNG",
+           "ReplayRNG"]
 __version__ = "0.1.0"

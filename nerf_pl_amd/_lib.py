@@ -44,7 +44,7 @@ SIGNATURES = {
     "nr_wgrad_b1": [_p, _p, _i64, _p, _p, _p],
     "nr_mlp_bwd": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
-    "nr_sm_workspace_bytes": [_i64],
+    "nr_sm_workspace_bytes": [_i64, _i64],
     "nr_wgrad": [_p, _p, _i64, _p, _p, _p],
     "nr_coarse_z": [_p, _p, _i64, _i, _i, _f, _p, _u64, _p, _p],
     "nr_composite_fwd": [_p, _i, _i, _p, _p, _p, _f, _u64, _i, _i64, _i, _i, _i, _p, _p, _p,
@@ -57,11 +57,16 @@ SIGNATURES = {
     "nr_adam_step": [_p, _p, _p, _p, _p, _i, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                      ctypes.c_double, ctypes.c_double, _i64, _p],
     "nr_mse_loss": [_p, _p, _p, _i64, _p, _p, _p],
+    "nr_opacity_loss": [_p, _p, _p, _i64, _i64, _f, _f, _p, _p, _p],
+    "nr_opacity_loss_bwd": [_p, _i64, _i64, _f, _p, _p, _p, _p, _p],
+    "nr_searchsorted": [_p, _p, _i64, _i64, _i64, _i64, _i, _p, _p],
+    "nr_searchsorted_f64": [_p, _p, _i64, _i64, _i64, _i64, _i, _p, _p],
     "nr_mse_loss_bwd": [_p, _p, _p, _i64, _p, _p, _p, _p],
     "nr_sm_normed_depth": [_p, _p, _p, _i64, _p, _p],
+    "nr_sm_normed_depth_bwd": [_p, _p, _p, _i64, _p, _p],
     "nr_sm_forward": [_p, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _f, _f, _i, _f, _i64, _p, _p,
                       _p],
-    "nr_sm_backward": [_p, _p, _i, _f, _f, _i, _i64, _p, _p],
+    "nr_sm_backward": [_p, _p, _i, _f, _f, _i, _i64, _i64, _p, _p, _p],
     "nr_sample_pdf": [_p, _i, _p, _p, _p, _p, _u64, _i64, _i, _p, _p, _p],
     "nr_embed": [_p, _i64, _i, _p, _p],
     "nr_pack": [_p, _p, _i64, _p, _p],

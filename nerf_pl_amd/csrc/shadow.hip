@@ -14,7 +14,17 @@
 //   sm_minmax_kernel    shadow_method_2: per-run min / max (one wave per run)
 //   sm_norm_kernel      shadow_method_2: min-max normalisation, clip
 //   backward: sm_bwd_reduce_kernel (per-run sums of the normalisation
-//   gradient) + sm_bwd_kernel (d loss / d camera depth).
+//   gradient) + sm_bwd_kernel (d loss / d camera depth, and each ray's
+//   contribution -d loss / d shadow difference to its gathered texel), then
+//   for gradients into the light map (train_efficient_sm.py --grad_on_light,
+//   :158-162) sm_scatter_kernel + sm_light_finish_kernel: the backward of the
+//   texel gather w_light.view(w, h)[v, u] (efficient_shadow_mapping.py:98) as
+//   a deterministic scatter-add -- every contribution converted to a 64-bit
+//   fixed-point integer at one power-of-two scale per call (chosen from the
+//   largest |contribution| so that no sum can overflow) and added with integer
+//   atomics, which are associative: the texel sums do not depend on the order
+//   the atomics land in, and they are exact to ~2^-60 of the largest term
+//   (the reference's index_put_ accumulates in fp32, ray by ray).
 //
 // Arithmetic follows the reference's fp32 op order; the 3x3 products that set
 // up the run's transform (M_L^-1 M, M_L^-1 (O - L)) are formed in double and
@@ -46,18 +56,30 @@ __device__ __forceinline__ float rowdot(const float* p, const float* row) {
     return nr_add(nr_add(nr_mul(p[0], row[0]), nr_mul(p[1], row[1])), nr_mul(p[2], row[2]));
 }
 
-// workspace layout (per ray): run start, shadow difference, projection
-// z-row, normed-depth denominator, per-run [min, max] and backward sums
+// workspace layout: per ray the run start, shadow difference, projection
+// z-row, normed-depth denominator, per-run [min, max] and backward sums, the
+// gathered texel and the texel-gradient contribution; then (8-byte aligned)
+// the largest |contribution| and, per light texel, a 64-bit fixed-point
+// accumulator and a non-finite flag
 struct SmWs {
     int32_t* run; float* t; float* proj2; float* normp; float* mm; float* sums;
+    int32_t* key; float* c; uint32_t* cmax; unsigned long long* acc; int32_t* flag;
 };
-__host__ __device__ inline SmWs sm_ws(void* base, int64_t n) {
+__host__ __device__ inline int64_t sm_ray_words(int64_t n) { return (12 * n + 1) & ~(int64_t)1; }
+__host__ __device__ inline SmWs sm_ws(void* base, int64_t n, int64_t n_light) {
     SmWs w;
     w.run = reinterpret_cast<int32_t*>(base);
     float* f = reinterpret_cast<float*>(base) + n;
     w.t = f; w.proj2 = f + n; w.normp = f + 2 * n; w.mm = f + 3 * n; w.sums = f + 5 * n;
+    w.key = reinterpret_cast<int32_t*>(f + 9 * n);
+    w.c = f + 10 * n;
+    w.cmax = reinterpret_cast<uint32_t*>(base) + sm_ray_words(n);
+    w.acc = reinterpret_cast<unsigned long long*>(w.cmax + 2);
+    w.flag = reinterpret_cast<int32_t*>(w.acc + n_light);
     return w;
 }
+// bytes of the zero-initialised tail (cmax, acc, flag)
+__host__ inline int64_t sm_tail_bytes(int64_t n_light) { return 8 + 12 * n_light; }
 
 struct SmArgs {
     const float* pixels; const float* depth; const float* eye; const float* cams; int per_ray;
@@ -150,8 +172,10 @@ __global__ void __launch_bounds__(256) sm_project_kernel(SmArgs a) {
     // get_projected_depths (:84-101): clamp, truncate, gather w_light.view(w, h)[v, u]
     const float uc = fminf((float)(a.res_w - 1), fmaxf(0.f, ul));
     const float vc = fminf((float)(a.res_h - 1), fmaxf(0.f, vl));
-    const float wlb = a.light_w[(int64_t)(int)vc * a.res_h + (int)uc];
+    const int key = (int)vc * a.res_h + (int)uc;
+    const float wlb = a.light_w[key];
     const float d = nr_sub(wl, wlb);
+    a.ws.key[i] = key;
     a.ws.t[i] = d;
     a.ws.proj2[i] = proj2;
     a.ws.normp[i] = normp;
@@ -202,8 +226,8 @@ __global__ void __launch_bounds__(256) sm_norm_kernel(SmArgs a) {
 }
 
 struct SmBwdArgs {
-    const float* g_out; int method; float delta, epsilon; int sigmoid; int n;
-    SmWs ws; float* g_depth;
+    const float* g_out; int method; float delta, epsilon; int sigmoid; int n; int n_light;
+    SmWs ws; float* g_depth; float* g_light;
 };
 
 __device__ __forceinline__ float gsum3(const float* g, int i) {
@@ -261,9 +285,7 @@ __global__ void __launch_bounds__(256) sm_bwd_reduce_kernel(SmBwdArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(256) sm_bwd_kernel(SmBwdArgs a) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
+__device__ float sm_bwd_ray(const SmBwdArgs& a, int i) {
     float gt;
     if (a.method == 1) {
         // clip -> max(x/delta, eps) -> /delta   (torch.maximum splits ties)
@@ -285,8 +307,55 @@ __global__ void __launch_bounds__(256) sm_bwd_kernel(SmBwdArgs a) {
         if (t == mn) gt += (-su[0]) / su[2] + (-su[1]) / su[2];
         if (t == mx) gt += su[1] / su[3];
     }
-    // wl = w * proj2 + Q2, w = depth / normp   (d w_light_bounded = 0: index)
-    a.g_depth[i] = nr_mul(gt, a.ws.proj2[i]) / a.ws.normp[i];
+    return gt;   // d loss / d (wl - w_light_bounded)
+}
+
+__global__ void __launch_bounds__(256) sm_bwd_kernel(SmBwdArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = i < a.n;
+    const float gt = in ? sm_bwd_ray(a, i) : 0.f;
+    // wl = w * proj2 + Q2, w = depth / normp   (the texel index carries no gradient)
+    if (in && a.g_depth) a.g_depth[i] = nr_mul(gt, a.ws.proj2[i]) / a.ws.normp[i];
+    if (a.g_light) {
+        // diff = wl - w_light_bounded: the gathered texel receives -gt
+        const float c = -gt;
+        if (in) a.ws.c[i] = c;
+        float m = (in && __builtin_isfinite(c)) ? fabsf(c) : 0.f;
+        m = wmax(m);      // every lane of the wave takes part
+        if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(a.ws.cmax, __float_as_uint(m));
+    }
+}
+
+// fixed-point scale of the scatter: 2^(62 - E - L) with max|c| < 2^E and
+// n < 2^L, so that |sum| < n max|c| stays below 2^62
+__device__ __forceinline__ int sm_fix_exp(uint32_t cmax_bits, int n) {
+    int e;
+    (void)frexpf(__uint_as_float(cmax_bits), &e);
+    const int l = 64 - __clzll((unsigned long long)n);
+    return 62 - e - l;
+}
+
+__global__ void __launch_bounds__(256) sm_scatter_kernel(SmBwdArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t mb = *a.ws.cmax;
+    const float c = a.ws.c[i];
+    const int k = a.ws.key[i];
+    if (!__builtin_isfinite(c)) { a.ws.flag[k] = 1; return; }
+    if (mb == 0u || c == 0.f) return;
+    const long long q = __double2ll_rn(ldexp((double)c, sm_fix_exp(mb, a.n)));
+    atomicAdd(a.ws.acc + k, (unsigned long long)q);
+}
+
+__global__ void __launch_bounds__(256) sm_light_finish_kernel(SmBwdArgs a) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.n_light) return;
+    const uint32_t mb = *a.ws.cmax;
+    float g = 0.f;
+    if (a.ws.flag[k]) g = __builtin_nanf("");
+    else if (mb != 0u)
+        g = (float)ldexp((double)(long long)a.ws.acc[k], -sm_fix_exp(mb, a.n));
+    a.g_light[k] = g;
 }
 
 __global__ void __launch_bounds__(256) sm_normed_kernel(const float* __restrict__ M,
@@ -301,9 +370,25 @@ __global__ void __launch_bounds__(256) sm_normed_kernel(const float* __restrict_
     out[i] = depth[i] / nr_add(norm, kEps);
 }
 
+// its backward: d/d depth of depth / (|M p| + 1e-5) (torch's DivBackward: g / b)
+__global__ void __launch_bounds__(256) sm_normed_bwd_kernel(const float* __restrict__ M,
+                                                            const float* __restrict__ pixels,
+                                                            const float* __restrict__ g, int n,
+                                                            float* __restrict__ g_depth) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float p[3] = {pixels[(size_t)i * 3], pixels[(size_t)i * 3 + 1], pixels[(size_t)i * 3 + 2]};
+    const float c0 = rowdot(p, M), c1 = rowdot(p, M + 3), c2 = rowdot(p, M + 6);
+    const float norm = sqrtf(nr_add(nr_add(nr_mul(c0, c0), nr_mul(c1, c1)), nr_mul(c2, c2)));
+    g_depth[i] = g[i] / nr_add(norm, kEps);
+}
+
 }  // namespace
 
-NR_API int64_t nr_sm_workspace_bytes(int64_t n) { return n * 9 * 4; }
+NR_API int64_t nr_sm_workspace_bytes(int64_t n, int64_t n_light) {
+    if (n < 0 || n_light < 0) return -1;
+    return sm_ray_words(n) * 4 + sm_tail_bytes(n_light);
+}
 
 NR_API int nr_sm_normed_depth(const float* camera, const float* pixels, const float* depth,
                               int64_t n, float* out, void* stream) {
@@ -313,6 +398,17 @@ NR_API int nr_sm_normed_depth(const float* camera, const float* pixels, const fl
     sm_normed_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
         camera, pixels, depth, (int)n, out);
     NR_LAUNCH_CHECK("nr_sm_normed_depth");
+    return 0;
+}
+
+NR_API int nr_sm_normed_depth_bwd(const float* camera, const float* pixels, const float* g_out,
+                                  int64_t n, float* g_depth, void* stream) {
+    NR_REQUIRE(n >= 0 && n < ((int64_t)1 << 31), "nr_sm_normed_depth_bwd: bad size");
+    if (n == 0) return 0;
+    NR_REQUIRE(camera && pixels && g_out && g_depth, "nr_sm_normed_depth_bwd: null pointer");
+    sm_normed_bwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        camera, pixels, g_out, (int)n, g_depth);
+    NR_LAUNCH_CHECK("nr_sm_normed_depth_bwd");
     return 0;
 }
 
@@ -331,7 +427,8 @@ NR_API int nr_sm_forward(const float* pixels, const float* depth, const float* e
                workspace && out, "nr_sm_forward: null pointer");
     hipStream_t st = (hipStream_t)stream;
     SmArgs a{pixels, depth, eye, cameras, per_ray, light_camera, light_eye, light_w, res_w,
-             res_h, method, delta, epsilon, sigmoid, out_eps, (int)n, sm_ws(workspace, n), out};
+             res_h, method, delta, epsilon, sigmoid, out_eps, (int)n,
+             sm_ws(workspace, n, (int64_t)res_w * res_h), out};
     sm_runs_kernel<<<1, 1024, 0, st>>>(eye, per_ray, (int)n, a.ws.run);
     const unsigned blocks = (unsigned)((n + 255) / 256);
     sm_project_kernel<<<blocks, 256, 0, st>>>(a);
@@ -344,16 +441,37 @@ NR_API int nr_sm_forward(const float* pixels, const float* depth, const float* e
 }
 
 NR_API int nr_sm_backward(const float* g_out, void* workspace, int method, float delta,
-                          float epsilon, int sigmoid, int64_t n, float* g_depth, void* stream) {
+                          float epsilon, int sigmoid, int64_t n, int64_t n_light, float* g_depth,
+                          float* g_light_w, void* stream) {
     NR_REQUIRE(n >= 0 && n < ((int64_t)1 << 31), "nr_sm_backward: bad size");
+    NR_REQUIRE(n_light > 0 && n_light < ((int64_t)1 << 31), "nr_sm_backward: bad light map size");
     NR_REQUIRE(method == 1 || method == 2, "nr_sm_backward: method must be 1 or 2");
-    if (n == 0) return 0;
-    NR_REQUIRE(g_out && workspace && g_depth, "nr_sm_backward: null pointer");
     hipStream_t st = (hipStream_t)stream;
-    SmBwdArgs a{g_out, method, delta, epsilon, sigmoid, (int)n, sm_ws(workspace, n), g_depth};
+    if (n == 0) {
+        // no camera rays: the light map receives no gradient
+        if (g_light_w && hipMemsetAsync(g_light_w, 0, (size_t)n_light * 4, st) != hipSuccess) {
+            nr_set_error("nr_sm_backward: memset failed");
+            return NR_EINVAL;
+        }
+        return 0;
+    }
+    NR_REQUIRE(g_out && workspace && (g_depth || g_light_w), "nr_sm_backward: null pointer");
+    SmBwdArgs a{g_out, method, delta, epsilon, sigmoid, (int)n, (int)n_light,
+                sm_ws(workspace, n, n_light), g_depth, g_light_w};
     const unsigned blocks = (unsigned)((n + 255) / 256);
+    if (g_light_w) {
+        const hipError_t e = hipMemsetAsync(a.ws.cmax, 0, (size_t)sm_tail_bytes(n_light), st);
+        if (e != hipSuccess) {
+            nr_set_error("nr_sm_backward: memset failed: %s", hipGetErrorString(e));
+            return (int)e;
+        }
+    }
     if (method == 2) sm_bwd_reduce_kernel<<<blocks, 256, 0, st>>>(a);
     sm_bwd_kernel<<<blocks, 256, 0, st>>>(a);
+    if (g_light_w) {
+        sm_scatter_kernel<<<blocks, 256, 0, st>>>(a);
+        sm_light_finish_kernel<<<(unsigned)((n_light + 255) / 256), 256, 0, st>>>(a);
+    }
     NR_LAUNCH_CHECK("nr_sm_backward");
     return 0;
 }

@@ -117,7 +117,49 @@ class GradAllReducer:
         self._hooks = []
 
 
-def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None):
+class _GatherRows(torch.autograd.Function):
+    """All-gather of equal padded row slices; its backward is the matching
+    reduce-scatter (sum): rank r's slice receives the sum over ranks of the
+    gradient of its rows, so after the usual parameter-gradient average every
+    rank holds the gradient of the mean loss, as if each had rendered every
+    row itself (the reference's replicated light render under DDP)."""
+
+    @staticmethod
+    def forward(ctx, buf, world, group):
+        ctx.world, ctx.group = world, group
+        full = torch.empty((world * buf.shape[0],) + tuple(buf.shape[1:]), dtype=buf.dtype,
+                           device=buf.device)
+        dist.all_gather_into_tensor(full, buf.contiguous(), group=group)
+        return full
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        per = g.shape[0] // ctx.world
+        if dist.get_backend(ctx.group) == "nccl":
+            out = torch.empty((per,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
+            dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=ctx.group)
+        else:       # gloo has no reduce-scatter: sum everything, keep the own slice
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=ctx.group)
+            rank = dist.get_rank(ctx.group)
+            out = g[rank * per:(rank + 1) * per].clone()
+        return out, None, None
+
+
+def _check_signature(part, group):
+    """Every rank must gather the same keys with the same trailing shapes and
+    dtypes (e.g. the same N_importance); a mismatch would pair different
+    tensors in the collectives or hang.  Raises on all ranks alike."""
+    sig = sorted((k, None if v is None else (tuple(v.shape[1:]), str(v.dtype)))
+                 for k, v in part.items())
+    sigs = [None] * dist.get_world_size(group)
+    dist.all_gather_object(sigs, sig, group=group)
+    if any(s != sigs[0] for s in sigs):
+        raise RuntimeError("sharded_map: ranks produced different outputs "
+                           f"(keys / trailing shapes / dtypes): {sigs}")
+
+
+def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None, check=True):
     """Row-sharded evaluation of ``fn`` over the ranks of ``group``: rank r
     applies ``fn`` to its contiguous slice of ``x`` (ceil(n / world) rows, the
     last slice shorter) and every rank receives the whole result, each output
@@ -126,10 +168,15 @@ def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None):
     slices).  ``rank_args(lo, hi)`` may supply extra keyword arguments for the
     rank's slice (e.g. a replay RNG holding the slice's random draws).
 
+    Outputs that require grad stay differentiable: the gather's backward is a
+    reduce-scatter (``_GatherRows``).  ``check`` first all-gathers each rank's
+    output signature and raises if they differ.
+
     Used for config 5's light image (SURVEY 8e "phase 2"): the reference
     renders the full light image on every rank (train_efficient_sm.py:158-168);
     sharding it divides that work by the world size at the cost of gathering
-    ~B floats per output (64 KB per map at 128^2)."""
+    ~B floats per output (64 KB per map at 128^2) and, with --grad_on_light,
+    reduce-scattering their gradients."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n = x.shape[0]
@@ -139,13 +186,21 @@ def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None):
         part = fn(x[lo:hi], **(rank_args(lo, hi) if rank_args else {}))
     else:       # an empty slice still takes part in every collective (same keys)
         part = fn(x[n - 1:n], **(rank_args(n - 1, n) if rank_args else {}))
+    if check:
+        _check_signature(part, group)
     out = {}
     for k in sorted(part):
         v = part[k]
         if v is None:
             out[k] = None
             continue
-        v = v.detach()[: hi - lo]
+        v = v[: hi - lo]
+        pad = per - v.shape[0]
+        if v.requires_grad and torch.is_grad_enabled():
+            buf = torch.cat([v, v.new_zeros((pad,) + tuple(v.shape[1:]))]) if pad else v
+            out[k] = _GatherRows.apply(buf, world, group)[:n]
+            continue
+        v = v.detach()
         buf = torch.zeros((per,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
         buf[: v.shape[0]] = v
         full = torch.empty((world * per,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)

@@ -18,12 +18,17 @@ from . import ops, packing
 from ._lib import call, stream_of
 
 
-@functools.lru_cache(maxsize=None)
+@functools.lru_cache(maxsize=4)
 def _wgrad_workspace(device_index: int, stream: int = 0) -> torch.Tensor:
     """Split-K slab workspace of the weight gradient, one per (device, stream):
     backward passes enqueued on different streams never share slabs.  The
     size is the library's bound over every launch shape (~604 MB; the slabs a
-    launch uses depend only on the task list, not on n)."""
+    launch uses depend only on the task list, not on n).  At most 4 are kept
+    (least recently used evicted): a workspace is allocated while its stream is
+    current, so once evicted the caching allocator hands its memory only to
+    later work on that same stream, which runs after the kernels still using
+    it -- code that creates side streams per iteration cannot pin unbounded
+    device memory."""
     from ._lib import lib
     nbytes = int(lib().nr_wgrad_workspace_bytes(0))
     return torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", device_index))

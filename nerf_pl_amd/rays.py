@@ -150,21 +150,50 @@ class RaySampler:
     reference's ray buffer + ``DataLoader(shuffle=True, batch_size=B)``
     (train.py:89-94): each epoch is a random permutation of all pixels of all
     poses (torch.randperm on the device), each batch is produced by one
-    ``nr_gen_rays`` launch that also gathers the target colours."""
+    ``nr_gen_rays`` launch that also gathers the target colours.
 
-    def __init__(self, c2w, H, W, focal, near, far, rgb_pool=None, ndc=False, seed=0):
+    Data-parallel runs partition every epoch like the ``DistributedSampler``
+    that Lightning's DDP backend installs (train.py:175): the same
+    permutation on every rank (generator seeded ``seed + epoch``, identical
+    across ranks), padded with its head to a multiple of ``world``, and rank r
+    takes ``perm[r::world]`` -- the ranks' batches are disjoint and together
+    cover the epoch.  An epoch ends when the rank's shard cannot fill another
+    batch (the remainder is dropped)."""
+
+    def __init__(self, c2w, H, W, focal, near, far, rgb_pool=None, ndc=False, seed=0, rank=0,
+                 world=1):
+        if not 0 <= rank < world:
+            raise ValueError(f"RaySampler: rank {rank} outside world {world}")
         self.c2w = c2w
         self.H, self.W, self.focal, self.near, self.far = H, W, focal, near, far
         self.rgb_pool, self.ndc = rgb_pool, ndc
         self.total = c2w.reshape(-1, 12).shape[0] * H * W
-        self.gen = torch.Generator(device=c2w.device).manual_seed(seed)
-        self.perm, self.pos = None, 0
+        self.seed, self.rank, self.world = seed, rank, world
+        self.device = c2w.device
+        self.epoch, self.shard, self.pos = -1, None, 0
+
+    def _new_epoch(self):
+        self.epoch += 1
+        gen = torch.Generator(device=self.device).manual_seed(self.seed + self.epoch)
+        perm = torch.randperm(self.total, device=self.device, generator=gen)
+        pad = (-self.total) % self.world          # DistributedSampler(drop_last=False)
+        if pad:
+            perm = torch.cat([perm, perm[:pad]])
+        self.shard = perm[self.rank::self.world]
+        self.pos = 0
+
+    def next_indices(self, batch: int):
+        """Global pixel indices of the next batch (pose*H*W + row*W + col)."""
+        if self.shard is None or self.pos + batch > self.shard.shape[0]:
+            self._new_epoch()
+            if batch > self.shard.shape[0]:
+                raise ValueError(f"RaySampler: batch {batch} exceeds the rank's "
+                                 f"{self.shard.shape[0]} rays per epoch")
+        sel = self.shard[self.pos:self.pos + batch]
+        self.pos += batch
+        return sel
 
     def next(self, batch: int):
-        if self.perm is None or self.pos + batch > self.total:
-            self.perm = torch.randperm(self.total, device=self.c2w.device, generator=self.gen)
-            self.pos = 0
-        sel = self.perm[self.pos:self.pos + batch]
-        self.pos += batch
+        sel = self.next_indices(batch)
         return generate_rays(self.c2w, self.H, self.W, self.focal, self.near, self.far, sel,
                              self.ndc, rgb_pool=self.rgb_pool)

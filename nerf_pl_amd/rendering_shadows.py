@@ -12,7 +12,9 @@ train_efficient_sm.py), executed by the HIP kernels.
 * ``efficient_sm(...)`` -- :359-482: shadow maps of the camera depths against
   the light's depth map (``nr_sm_forward`` / ``nr_sm_backward``); the
   reference's per-ray ``torch.equal`` run-splitting loop (:377-396) becomes a
-  device scan.
+  device scan.  Differentiable in the camera depths and, when the light render
+  was run with gradients (``--grad_on_light``, train_efficient_sm.py:158-162),
+  in the light depths too.
 
 ``chunk`` and ``white_back`` are accepted and unused (the reference ignores
 ``white_back`` here too); ``rng`` is the added keyword of ``rendering.py``.
@@ -37,7 +39,7 @@ def _disp(depth, opac):
 
 def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=0, noise_std=1,
                 N_importance=0, chunk=1024 * 32, white_back=False, test_time=False,
-                were_gradients_computed=True, *, rng=None):
+                were_gradients_computed=True, *, rng=None, _capture=None):
     del chunk, white_back, were_gradients_computed
     _check_embeddings(embeddings, models)
     rays = ops._dev(rays, "rays", 8)
@@ -49,6 +51,8 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
     u1 = rng.rand((n_rays, N_samples), dev) if perturb > 0 else None
     z_c = ops.coarse_z(rays, N_samples, use_disp, perturb, u=u1, seed=seed)
     noise_c = rng.randn((n_rays, N_samples), dev)
+    cap = _capture if _capture is not None else {}
+    cap["z_coarse"] = z_c
     result = {}
     if test_time:
         with torch.no_grad():
@@ -70,6 +74,8 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
         jit = rng.rand((n_rays, N_importance), dev)
         _, z_f = ops.sample_pdf(w_c.detach(), rays, N_importance, u=u, jitter=jit, seed=seed,
                                 z_coarse=z_c, merge=True)
+        cap["weights_coarse"] = w_c
+        cap["z_fine"] = z_f
         s_f = N_samples + N_importance
         noise_f = rng.randn((n_rays, s_f), dev)
         sig_f = mlp_apply(models[1], rays=rays, z=z_f, spr=s_f, sigma_only=True)
@@ -84,23 +90,29 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
 def render_rays_sharded(models, embeddings, rays, N_samples=64, use_disp=False, perturb=0,
                         noise_std=1, N_importance=0, chunk=1024 * 32, white_back=False,
                         test_time=False, *, group=None, rng=None, rng_for_rows=None):
-    """The no_grad light-image render of train_efficient_sm.py:158-168 split
-    over the ranks of ``group`` (SURVEY 8e, config 5 "phase 2"): each rank
-    renders its contiguous slice of ``rays`` and all-gathers every output map
+    """The light-image render of train_efficient_sm.py:158-168 split over the
+    ranks of ``group`` (SURVEY 8e, config 5 "phase 2"): each rank renders its
+    contiguous slice of ``rays`` and all-gathers every output map
     (``distributed.sharded_map``), instead of every rank rendering the whole
     image as the reference does.  Per-ray results do not depend on the other
     rays of a call, so with the same random draws the gathered maps equal the
     replicated render bit for bit; ``rng_for_rows(lo, hi)`` supplies the draws
     of rows lo..hi (e.g. a ReplayRNG of the sliced tensors), else each rank
     draws from ``rng`` (default: its own Philox stream -- distribution-equivalent,
-    like the reference's per-process generators)."""
+    like the reference's per-process generators).
+
+    Follows the caller's grad mode like the reference: under ``torch.no_grad()``
+    (the default light render, :164-168) nothing is recorded; with gradients
+    enabled (``--grad_on_light``, :158-162) the gathered maps stay
+    differentiable and their gradients are reduce-scattered back to the rank
+    that rendered each row.  ``N_importance`` must be the same on every rank
+    (checked: ``sharded_map`` raises on mismatched outputs)."""
     from .distributed import sharded_map
 
     def fn(r, rng=rng):
-        with torch.no_grad():
-            return render_rays(models, embeddings, r.contiguous(), N_samples, use_disp, perturb,
-                               noise_std, N_importance, chunk, white_back, test_time, False,
-                               rng=rng)
+        return render_rays(models, embeddings, r.contiguous(), N_samples, use_disp, perturb,
+                           noise_std, N_importance, chunk, white_back, test_time, False,
+                           rng=rng)
     extra = (lambda lo, hi: {"rng": rng_for_rows(lo, hi)}) if rng_for_rows else None
     return sharded_map(fn, rays, group, extra)
 

@@ -63,8 +63,24 @@ def _cases():
         ("nr_mse_loss", [N, N, N, 5, N, N, N], NR_EINVAL),
         ("nr_mse_loss_bwd", [N, N, N, -1, N, N, N, N], NR_EINVAL),
         ("nr_mse_loss_bwd", [N, N, N, 5, N, N, N, N], NR_EINVAL),
+        ("nr_opacity_loss", [N, N, N, 9, 8, 0.4, 2000.0, N, N, N], NR_EINVAL),   # n_t > n_o
+        ("nr_opacity_loss", [N, N, N, 4, 8, 0.4, 2000.0, N, N, N], NR_EINVAL),
+        ("nr_opacity_loss_bwd", [N, 4, 8, 0.4, N, N, N, N, N], NR_EINVAL),
+        ("nr_searchsorted", [N, N, 3, 4, 2, 5, 0, N, N], NR_EINVAL),     # 3 vs 2 rows
+        ("nr_searchsorted", [N, N, -1, 4, 2, 5, 0, N, N], NR_EINVAL),
+        ("nr_searchsorted", [N, N, 0, 4, 0, 5, 0, N, N], 0),
+        ("nr_searchsorted", [N, N, 2, 4, 2, 5, 1, N, N], NR_EINVAL),     # null pointers
+        ("nr_searchsorted_f64", [N, N, 2, 4, 2, 5, 1, N, N], NR_EINVAL),
         ("nr_sm_normed_depth", [N, N, N, -1, N, N], NR_EINVAL),
-        ("nr_sm_backward", [N, N, 1, 1e-3, 1e-3, 0, -1, N, N], NR_EINVAL),
+        ("nr_sm_normed_depth", [N, N, N, 5, N, N], NR_EINVAL),
+        ("nr_sm_normed_depth_bwd", [N, N, N, -1, N, N], NR_EINVAL),
+        ("nr_sm_normed_depth_bwd", [N, N, N, 0, N, N], 0),
+        ("nr_sm_normed_depth_bwd", [N, N, N, 5, N, N], NR_EINVAL),
+        ("nr_sm_backward", [N, N, 1, 1e-3, 1e-3, 0, -1, 16, N, N, N], NR_EINVAL),
+        ("nr_sm_backward", [N, N, 1, 1e-3, 1e-3, 0, 4, 0, N, N, N], NR_EINVAL),   # no light map
+        ("nr_sm_backward", [N, N, 3, 1e-3, 1e-3, 0, 4, 16, N, N, N], NR_EINVAL),  # bad method
+        ("nr_sm_backward", [N, N, 1, 1e-3, 1e-3, 0, 0, 16, N, N, N], 0),
+        ("nr_sm_backward", [N, N, 1, 1e-3, 1e-3, 0, 4, 16, N, N, N], NR_EINVAL),  # no output
         ("nr_sm_forward", [N, N, N, N, 0, N, N, N, 128, 128, 2, 1e-3, 1e-3, 0, 1e-5, -1, N, N, N],
          NR_EINVAL),
     ]

@@ -173,3 +173,114 @@ def test_sharded_map_gathers_every_row():
             assert none is None
             lo, hi = min(n, rank * per), min(n, (rank + 1) * per)
             assert seen == [(hi - lo, (lo, hi))] if hi > lo else seen == [(1, (n - 1, n))]
+
+
+def _shard_grad_worker(rank, world, port, q, n, mismatch):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nerf_pl_amd.distributed import sharded_map
+        w = torch.nn.Parameter(torch.linspace(0.5, 1.5, 3))
+        x = torch.arange(n * 3, dtype=torch.float32).view(n, 3)
+
+        def fn(xs):
+            out = {"y": (xs * w).sum(1)}
+            if mismatch and rank == 1:
+                out["extra"] = xs[:, 0]
+            return out
+        try:
+            out = sharded_map(fn, x)
+        except RuntimeError as e:
+            q.put((rank, "raised", str(e)))
+            return
+        # rank-dependent loss on the gathered rows (each rank's own camera batch)
+        coef = torch.arange(n, dtype=torch.float32) * (rank + 1)
+        (out["y"] * coef).sum().backward()
+        q.put((rank, "ok", w.grad.clone()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, target, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_sharded_map_backward_reduce_scatters():
+    """--grad_on_light with the light image sharded: the gathered rows stay
+    differentiable, and each rank's parameter gradient is what it gets from the
+    rows it rendered under every rank's loss -- so the all-reduced average
+    equals the reference's (every rank renders every row, DDP averages)."""
+    world, n = 2, 7
+    res = _run(world, _shard_grad_worker, n, False)
+    x = torch.arange(n * 3, dtype=torch.float32).view(n, 3)
+    per = (n + world - 1) // world
+    coef_sum = torch.arange(n, dtype=torch.float32) * sum(r + 1 for r in range(world))
+    total = torch.zeros(3)
+    for rank, status, g in res:
+        assert status == "ok"
+        lo, hi = rank * per, min(n, (rank + 1) * per)
+        exp = (coef_sum[lo:hi, None] * x[lo:hi]).sum(0)
+        torch.testing.assert_close(g, exp, rtol=1e-6, atol=1e-6)
+        total += g
+    # average over ranks == mean over ranks of the replicated per-rank gradients
+    rep = [(torch.arange(n, dtype=torch.float32)[:, None] * (r + 1) * x).sum(0)
+           for r in range(world)]
+    torch.testing.assert_close(total / world, sum(rep) / world, rtol=1e-6, atol=1e-6)
+
+
+def test_sharded_map_rejects_mismatched_outputs():
+    """ranks drawing different N_importance (train_efficient_sm.py
+    Light_N_importance == -1) produce different keys; sharded_map raises on
+    every rank instead of pairing the wrong tensors or hanging."""
+    res = _run(2, _shard_grad_worker, 5, True)
+    for rank, status, msg in res:
+        assert status == "raised" and "different outputs" in msg, (rank, status, msg)
+
+
+def _sampler_worker(rank, world, port, q, total, batch, steps):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nerf_pl_amd.rays import RaySampler
+        # CPU poses: only the index partitioning is exercised (no ray generation)
+        s = RaySampler(torch.zeros(total, 3, 4), 1, 1, 1.0, 2.0, 6.0, seed=7, rank=rank,
+                       world=world)
+        q.put((rank, [s.next_indices(batch).clone() for _ in range(steps)], s.epoch))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ray_sampler_partitions_epochs_like_distributed_sampler():
+    """SURVEY 8e / train.py:89-94 under DDP: one permutation per epoch shared by
+    every rank, rank r taking perm[r::world] -- the ranks' batches are
+    disjoint within an epoch and together cover it; the next epoch reshuffles."""
+    world, total, batch = 2, 96, 12
+    steps = total // world // batch          # one epoch
+    res = _run(world, _sampler_worker, total, batch, steps + 1)
+    ep = []
+    for rank, batches, epoch in res:
+        assert epoch == 1
+        ep.append(torch.cat(batches[:steps]))
+        assert all(b.shape == (batch,) for b in batches)
+    a, b = ep
+    assert not set(a.tolist()) & set(b.tolist())                 # disjoint
+    assert sorted(a.tolist() + b.tolist()) == list(range(total))  # cover the epoch
+    # identical to torch.utils.data.DistributedSampler's partition of the epoch
+    g = torch.Generator().manual_seed(7)
+    perm = torch.randperm(total, generator=g)
+    for rank, e in enumerate(ep):
+        torch.testing.assert_close(e, perm[rank::world], rtol=0, atol=0)
+    # the second epoch is a different permutation
+    assert not torch.equal(res[0][1][steps], res[0][1][0])

@@ -82,3 +82,61 @@ def test_loss_rejects_bad_inputs():
         MSELoss()({"rgb_coarse": torch.rand(8, 3)}, t)
     with pytest.raises(ValueError):
         MSELoss()({"rgb_coarse": torch.rand(0, 3, device=DEV)}, torch.rand(0, 3, device=DEV))
+
+
+def test_loss_checks_the_target():
+    """a CPU or non-float32 target raises like torch's device /
+    dtype errors instead of handing the kernel a host pointer or misread bits;
+    a target that requires grad receives nn.MSELoss's gradient."""
+    from nerf_pl_amd.losses import MSELoss
+    x = {"rgb_coarse": torch.rand(8, 3, device=DEV), "rgb_fine": torch.rand(8, 3, device=DEV)}
+    with pytest.raises(ValueError, match="device"):
+        MSELoss()(x, torch.rand(8, 3))
+    with pytest.raises(ValueError, match="float32"):
+        MSELoss()(x, torch.rand(8, 3, device=DEV, dtype=torch.float64))
+    with pytest.raises(ValueError, match="float32"):
+        MSELoss()(x, torch.rand(8, 3, device=DEV).half())
+    t = torch.rand(8, 3, device=DEV, requires_grad=True)
+    a = x["rgb_coarse"].clone().requires_grad_(True)
+    b = x["rgb_fine"].clone().requires_grad_(True)
+    MSELoss()({"rgb_coarse": a, "rgb_fine": b}, t).backward()
+    t2 = t.detach().clone().requires_grad_(True)
+    a2, b2 = a.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    (torch.nn.functional.mse_loss(a2, t2) + torch.nn.functional.mse_loss(b2, t2)).backward()
+    for u, w in ((a, a2), (b, b2), (t, t2)):
+        torch.testing.assert_close(u.grad, w.grad, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("n_t,n_o,fine,seed", [(512, 4096, True, 0), (300, 300, False, 1),
+                                               (7, 64, True, 2)])
+def test_opacity_loss_matches_reference(n_t, n_o, fine, seed):
+    """losses.py:28-73 OpactiyLoss, as train_efficient_sm.py:191 calls it: the
+    light render's opacities indexed by the camera batch's shadow pixels."""
+    from oracle import nerf_oracle as O
+    from nerf_pl_amd.losses import loss_dict
+    g = torch.Generator().manual_seed(seed)
+    tgt = torch.rand(n_t, 3, generator=g)
+    res = {"opacity_coarse": torch.rand(n_o, generator=g)}
+    if fine:
+        res["opacity_fine"] = torch.rand(n_o, generator=g)
+    ref_in = {k: v.clone().requires_grad_(True) for k, v in res.items()}
+    ref = O.opacity_loss(ref_in, tgt)
+    ref.backward()
+    dev_in = {k: v.to(DEV).requires_grad_(True) for k, v in res.items()}
+    got = loss_dict["opacity"]()(dev_in, tgt.to(DEV))
+    got.backward()
+    assert abs(got.item() - ref.item()) <= 1e-3 * 1e-4 * abs(ref.item()) + 1e-4
+    for k in res:
+        torch.testing.assert_close(dev_in[k].grad.cpu(), ref_in[k].grad, rtol=1e-5, atol=1e-9)
+
+
+def test_opacity_loss_empty_set_is_zero():
+    from nerf_pl_amd.losses import OpactiyLoss
+    tgt = torch.zeros(16, 3, device=DEV)          # no shadow pixel
+    o = {"opacity_coarse": torch.rand(32, device=DEV, requires_grad=True)}
+    loss = OpactiyLoss()(o, tgt)
+    assert loss.item() == 0.0
+    loss.backward()
+    assert (o["opacity_coarse"].grad == 0).all()
+    with pytest.raises(IndexError):
+        OpactiyLoss()({"opacity_coarse": torch.rand(8, device=DEV)}, torch.rand(9, 3, device=DEV))

@@ -43,8 +43,10 @@ def _worker(rank, world, port, q):
         from nerf_pl_amd import ReplayRNG
         from nerf_pl_amd import rendering_shadows as RS
         models, emb, rays, draws = _setup()
-        out = RS.render_rays_sharded(models, emb, rays, S, False, 1.0, 0.0, I, 32768, False,
-                                     rng_for_rows=lambda lo, hi: ReplayRNG([d[lo:hi] for d in draws]))
+        with torch.no_grad():      # the default light render (train_efficient_sm.py:164-168)
+            out = RS.render_rays_sharded(
+                models, emb, rays, S, False, 1.0, 0.0, I, 32768, False,
+                rng_for_rows=lambda lo, hi: ReplayRNG([d[lo:hi] for d in draws]))
         torch.cuda.synchronize()
         q.put((rank, {k: v.cpu() for k, v in out.items()}))
     finally:

@@ -30,59 +30,101 @@ def shadow_cfg(fx):
                 light_importance=int(c[3]),
                 method="shadow_method_1" if int(c[4]) == 1 else "shadow_method_2",
                 sigma_bias=float(c[5]), perturb=float(c[6]), noise_std=float(c[7]),
-                seeds=(int(c[8]), int(c[9])))
+                seeds=(int(c[8]), int(c[9])),
+                grad_on_light=len(c) > 10 and bool(c[10]))
 
 
-def run_oracle(fx, requires_grad=False):
+def fixture_draws(fx):
+    """The reference's random draws of a case, in call order: stored, or (the
+    cfg5-shaped cases) re-drawn from the recorded seed with the CPU generator
+    and checked against the recorded checksums."""
+    n = int(fx["n_draws"])
+    if "draws_seed" not in fx:
+        return [fx[f"draw{i}"] for i in range(n)]
+    torch.manual_seed(int(fx["draws_seed"]))
+    out = []
+    for i in range(n):
+        shape = tuple(int(v) for v in fx[f"draw{i}_shape"])
+        t = torch.randn(shape) if str(fx[f"draw{i}_kind"]) == "randn" else torch.rand(shape)
+        flat = t.reshape(-1).double()
+        got = np.array([float(flat.sum()), float((flat * flat).sum())] + flat[:8].tolist())
+        np.testing.assert_allclose(got, fx[f"draw{i}_sum"], rtol=1e-12, atol=0,
+                                   err_msg=f"re-drawn draw {i} differs from the reference's")
+        out.append(t.numpy())
+    return out
+
+
+def n_models(cfg):
+    return 2 if cfg["N_importance"] > 0 or cfg["light_importance"] > 0 else 1
+
+
+def run_oracle(fx, requires_grad=False, dtype=torch.float32):
     cfg = shadow_cfg(fx)
-    n_models = 2 if cfg["N_importance"] > 0 else 1
-    params = [O.make_params(s, sigma_bias=cfg["sigma_bias"]) for s in cfg["seeds"][:n_models]]
+    params = [{k: v.to(dtype) for k, v in O.make_params(s, sigma_bias=cfg["sigma_bias"]).items()}
+              for s in cfg["seeds"][:n_models(cfg)]]
     if requires_grad:
         params = [{k: v.requires_grad_(True) for k, v in p.items()} for p in params]
-    rng = O.ReplayRNG([fx[f"draw{i}"] for i in range(int(fx["n_draws"]))])
-    t = torch.from_numpy
-    cam = SO.render_rays(params, t(fx["rays"]), cfg["N_samples"], False, cfg["perturb"],
+    rng = O.ReplayRNG(fixture_draws(fx))
+    rng._queue = [q.to(dtype) for q in rng._queue]
+
+    def t(k):
+        return torch.from_numpy(fx[k]).to(dtype)
+    cam = SO.render_rays(params, t("rays"), cfg["N_samples"], False, cfg["perturb"],
                          cfg["noise_std"], cfg["N_importance"], rng=rng)
-    with torch.no_grad():
-        light = SO.render_rays(params, t(fx["light_rays"]), cfg["N_samples"], False,
+    with torch.set_grad_enabled(requires_grad and cfg["grad_on_light"]):
+        light = SO.render_rays(params, t("light_rays"), cfg["N_samples"], False,
                                cfg["perturb"], cfg["noise_std"], cfg["light_importance"],
                                rng=rng)
     assert rng.exhausted()
+    depths, light_depths = {}, {}
     for k in ("depth_coarse", "depth_fine"):
         if k in cam and requires_grad:
             cam[k].retain_grad()
-    depths = {k: cam[k] for k in ("depth_coarse", "depth_fine") if k in cam}
-    ppc = {"eye_pos": t(fx["eye_pos"]), "camera": t(fx["camera"])}
-    out = SO.efficient_sm(t(fx["pixels"]), t(fx["light_pixels"]), cam, light, ppc,
-                          t(fx["light_eye"]), t(fx["light_camera"]), (cfg["wh"], cfg["wh"]),
+            depths[k] = cam[k]
+        if k in light and light[k].requires_grad:
+            light[k].retain_grad()
+            light_depths[k] = light[k]
+    ppc = {"eye_pos": t("eye_pos"), "camera": t("camera")}
+    out = SO.efficient_sm(t("pixels"), t("light_pixels"), cam, light, ppc,
+                          t("light_eye"), t("light_camera"), (cfg["wh"], cfg["wh"]),
                           cfg["N_importance"] > 0, cfg["light_importance"] > 0, cfg["method"])
-    return cfg, params, cam, light, out, depths
+    return cfg, params, cam, light, out, depths, light_depths
 
 
 @pytest.mark.parametrize("case", CASES)
 def test_shadow_oracle_forward_matches(case):
     fx = load_shadow(case)
-    _, _, _, light, out, _ = run_oracle(fx)
+    with torch.no_grad():
+        _, _, _, light, out, _, _ = run_oracle(fx)
     for k, v in list(out.items()) + [("light_" + k, v) for k, v in light.items()]:
         ref = fx[k if k.startswith("light_") else f"out_{k}"]
         np.testing.assert_allclose(v.detach().numpy(), ref, rtol=1e-5,
                                    atol=1e-6 * max(1.0, float(np.abs(ref).max())), err_msg=k)
 
 
-@pytest.mark.parametrize("case", CASES)
-def test_shadow_oracle_gradients(case):
-    fx = load_shadow(case)
-    _, params, _, _, out, depths = run_oracle(fx, requires_grad=True)
-    tgt = torch.from_numpy(fx["target"])
+def _loss(out, fx, dtype=torch.float32):
+    tgt = torch.from_numpy(fx["target"]).to(dtype)
     loss = torch.mean((out["rgb_coarse"] - tgt) ** 2)
     if "rgb_fine" in out:
         loss = loss + torch.mean((out["rgb_fine"] - tgt) ** 2)
+    return loss
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if not c.startswith("cfg5")])
+def test_shadow_oracle_gradients(case):
+    """Gradients of the oracle's training step against the reference's: the
+    camera depths, (--grad_on_light) the light depths, and every parameter."""
+    fx = load_shadow(case)
+    cfg, params, _, _, out, depths, light_depths = run_oracle(fx, requires_grad=True)
+    assert bool(light_depths) == cfg["grad_on_light"]
+    loss = _loss(out, fx)
     assert loss.item() == pytest.approx(float(fx["loss"]), rel=1e-6)
     loss.backward()
-    for k, d in depths.items():
-        ref = fx[f"grad_{k}"]
-        np.testing.assert_allclose(d.grad.numpy(), ref, rtol=1e-4,
-                                   atol=1e-5 * max(1e-12, np.abs(ref).max()))
+    for pre, dd in (("grad_", depths), ("grad_light_", light_depths)):
+        for k, d in dd.items():
+            ref = fx[pre + k]
+            np.testing.assert_allclose(d.grad.numpy(), ref, rtol=1e-4,
+                                       atol=1e-5 * max(1e-12, np.abs(ref).max()), err_msg=pre + k)
     for m, p in enumerate(params):
         for name, v in p.items():
             key = f"grad{m}_{name}"
@@ -97,6 +139,16 @@ def test_shadow_oracle_gradients(case):
             else:
                 np.testing.assert_allclose(g[fx[key + "_idx"]], fx[key + "_val"], rtol=1e-3,
                                            atol=1e-4 * scale, err_msg=key)
+
+
+def test_cfg5_draws_redraw_from_seed():
+    """The cfg5-shaped fixtures do not store their 1.3M random draws: the CPU
+    generator re-draws them from the recorded seed (checksums must match)."""
+    for case in [c for c in CASES if c.startswith("cfg5")]:
+        fx = load_shadow(case)
+        assert "draws_seed" in fx
+        draws = fixture_draws(fx)
+        assert len(draws) == int(fx["n_draws"])
 
 
 def test_shadow_runs_split_like_reference():
