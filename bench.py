@@ -240,8 +240,29 @@ def install_timers(timer):
 _CPU_THREADS = None      # set for the single-thread row
 
 
+def host_cpus():
+    """CPUs this process may run on: os.cpu_count() (the machine), the
+    affinity mask, and the cgroup CPU quota (cpu.max) -- on the GPU boxes
+    os.cpu_count() reports the whole machine (256) while the container is
+    granted 16 CPUs of time, so 256 torch threads would only be throttled."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = total
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(total, aff, quota or total)
+    return dict(os_cpu_count=total, affinity=aff, cgroup_quota=quota, usable=usable)
+
+
 def _cpu_threads():
-    t = _CPU_THREADS or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    t = _CPU_THREADS or host_cpus()["usable"]
     torch.set_num_threads(t)
     return t
 
@@ -257,11 +278,14 @@ def _timed_loop(fn, budget_s, min_iters=2):
 
 
 def cpu_train(args, budget_s, rays_all, label):
-    """Oracle training steps (render_rays fwd + bwd + Adam) on b=256-ray batches."""
+    """Oracle training steps (render_rays fwd + bwd + Adam) on the workload's own
+    batch (args.batch rays: 4096 at cfg2), at least 2 steps; the single-thread
+    row times 256-ray batches (one 4096-ray step would take ~40 s
+    on one core)."""
     from oracle import nerf_oracle as O
     threads = _cpu_threads()
     torch.manual_seed(0)
-    b = 256
+    b = 256 if threads == 1 else args.batch
     params = [{k: v.requires_grad_(True) for k, v in O.make_params(s).items()} for s in (1, 2)]
     opt = torch.optim.Adam([p for d in params for p in d.values()], lr=5e-4)
 
@@ -275,6 +299,7 @@ def cpu_train(args, budget_s, rays_all, label):
         opt.step()
     n, el = _timed_loop(step, budget_s)
     return dict(value=n * b / el, unit="rays/s", cores=threads, kind="port",
+                host=host_cpus(),
                 sample=f"{n} oracle training steps x {b} rays ({label}, {args.n_samples}+"
                        f"{args.n_importance} samples, fwd+bwd+Adam) in {el:.1f} s, torch CPU "
                        f"{threads} threads")

@@ -76,6 +76,7 @@ def render_rays(models: List[Params], rays, N_samples=64, use_disp=False, pertur
     cap["weights_coarse"] = w_c
     if N_importance > 0:
         z_pdf = sample_pdf(rays, w_c[:, 1:-1], N_importance, rng).detach()
+        cap["z_pdf"] = z_pdf
         z_f, _ = torch.sort(torch.cat([z, z_pdf], -1), -1)
         cap["z_fine"] = z_f
         xyz_f = rays_o.unsqueeze(1) + rays_d.unsqueeze(1) * z_f.unsqueeze(2)

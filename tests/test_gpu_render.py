@@ -14,6 +14,7 @@ import torch
 
 from conftest import golden_cases, golden_cfg, golden_draws, load_golden
 from oracle import nerf_oracle as O
+from screening import pdf_flips
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -42,7 +43,9 @@ def run_ours(fx, cfg, models, grad=False):
 
 
 def screened_rays(fx, cfg, cap):
-    """Rays excluded from the tight comparison, with the reason checked."""
+    """Rays excluded from the tight comparison, each explained: a z_fine move
+    must come from reference importance samples whose u lies within 1e-5 of
+    one of the reference's CDF knots (screening.pdf_flips)."""
     bad = np.zeros(fx["rays"].shape[0], bool)
     ocap = {}
     params = [O.make_params(cfg["seeds"][0], sigma_bias=cfg["sigma_bias"]),
@@ -54,6 +57,10 @@ def screened_rays(fx, cfg, cap):
     if "z_fine" in cap:
         zf = cap["z_fine"].cpu().numpy()
         flip = np.abs(zf - ocap["z_fine"].numpy()).max(1) > 1e-4 * np.maximum(1, np.abs(zf).max(1))
+        moved, explained = pdf_flips(cap["z_fine"], ocap, golden_draws(fx)[-3])
+        assert not (flip & ~moved).any(), "z_fine differs although every importance depth matches"
+        assert not (moved & ~explained).any(), \
+            f"z_fine moved away from any CDF knot: rays {np.nonzero(moved & ~explained)[0][:8]}"
         bad |= flip
     return bad, ocap
 
