@@ -9,7 +9,10 @@ from __future__ import annotations
 import ctypes
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnerf_pl_amd.so")
+# NERF_PL_AMD_LIB: another build of the same ABI (tests/test_abi_asan.py loads the
+# host AddressSanitizer build through it)
+LIB_PATH = os.environ.get("NERF_PL_AMD_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libnerf_pl_amd.so")
 
 _p = ctypes.c_void_p
 _i = ctypes.c_int

@@ -3,6 +3,10 @@ target: "PSNR within 0.1 dB of the reference").
 
     python scripts/psnr_compare.py --impl ours        # on the MI355X box
     python scripts/psnr_compare.py --impl reference   # here only (imports /root/reference)
+    python scripts/psnr_compare.py --impl oracle      # on the MI355X box: the reference's
+        # algorithm (oracle/nerf_oracle.py, pinned bit-exact to the reference) in PyTorch
+        # fp32 on the GPU -- the reference as its authors ran it (PyTorch ops on a GPU,
+        # here hipBLAS GEMMs); test infrastructure used as the checker, not the product
 
 Both legs train the same NeRF pair (seeded parameters, oracle.make_params) with
 the reference's training step (train.py:103-117: render_rays 64+64, perturb 1,
@@ -120,7 +124,7 @@ def initial_params(seed: int, perturb_ulp: bool):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--impl", choices=["ours", "reference"], required=True)
+    ap.add_argument("--impl", choices=["ours", "reference", "oracle"], required=True)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--eval-every", type=int, default=250)
@@ -155,6 +159,40 @@ def main():
         def render(rays, test_time=False):
             return render_rays(models, emb, rays.to(dev), S, False, 1.0, 1.0, I, 32768, False,
                                test_time, rng=draws)
+    elif args.impl == "oracle":
+        from oracle import nerf_oracle as O
+        dev = torch.device("cuda", 0)
+        params = [{k: v.to(dev).requires_grad_(True)
+                   for k, v in initial_params(s, args.perturb_ulp).items()} for s in (101, 102)]
+
+        class _Holder(torch.nn.Module):      # parameters() / state_dict() for the harness
+            def __init__(self, p):
+                super().__init__()
+                self._p = p
+
+            def parameters(self, recurse=True):
+                return iter(self._p.values())
+
+            def state_dict(self, *a, **k):
+                return dict(self._p)
+
+            def load_state_dict(self, sd, *a, **k):
+                with torch.no_grad():
+                    for n, v in sd.items():
+                        self._p[n].copy_(v)
+        models = [_Holder(p) for p in params]
+
+        class _DevDraws:
+            def rand(self, shape):
+                return torch.rand(*shape).to(dev)
+
+            def randn(self, shape):
+                return torch.randn(*shape).to(dev)
+        odraws = _DevDraws()
+
+        def render(rays, test_time=False):
+            return O.render_rays(params, rays.to(dev), S, False, 1.0, 1.0, I, 32768, False,
+                                 test_time, rng=odraws)
     else:
         ref_nerf, ref_rendering = import_reference()
         dev = torch.device("cpu")
@@ -233,6 +271,8 @@ def main():
     if args.impl == "ours":
         from nerf_pl_amd import ops
         out["mlp_arithmetic"] = ops.MATH
+    elif args.impl == "oracle":
+        out["mlp_arithmetic"] = "torch fp32 (hipBLAS) -- the reference algorithm on the GPU"
     path = args.out or os.path.join(REPO, "profiles", "r01", f"psnr_{args.impl}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
