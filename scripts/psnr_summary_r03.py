@@ -1,0 +1,101 @@
+"""PSNR against the reference over draw seeds, round 3 (BASELINE.json target:
+"PSNR within 0.1 dB of the reference").
+
+Groups of scripts/psnr_compare.py runs (2000 steps, PSNR at 500/1000/1500/2000,
+fine rgb on 2 held-out views; unperturbed runs only):
+  f16x3      this package, default arithmetic   profiles/r03/psnr/f16x3_s*.json
+  fp32       this package, exact fp32 MFMA      profiles/r03/psnr/fp32_s*.json
+  ref_gpu    the reference's algorithm in PyTorch fp32 on the MI355X (the oracle,
+             pinned bit-exact to the reference; hipBLAS GEMMs)   profiles/r03/psnr/oracle_s*.json
+  ref_cpu    the reference itself, CPU, here    profiles/r01/psnr_reference_s*.json,
+             profiles/r02/psnr/reference_s*.json, profiles/r03/psnr/reference_s*.json
+Per checkpoint: each group's n / mean / std, and for every pair the difference
+of the means, its standard error (Welch), the 95% interval and whether that
+interval lies inside +-0.1 dB.  Writes profiles/r03/psnr/summary.json.
+
+    python scripts/psnr_summary_r03.py
+"""
+import glob
+import json
+import math
+import os
+import re
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STEPS = (500, 1000, 1500, 2000)
+
+
+def load(*patterns):
+    runs = {}
+    for pat in patterns:
+        for f in sorted(glob.glob(os.path.join(REPO, pat))):
+            d = json.load(open(f))
+            if d.get("perturb_ulp") or "eval_weights" in d or "psnr" not in d:
+                continue
+            seed = int(re.search(r"_s(\d+)", os.path.basename(f)).group(1))
+            runs[seed] = {p["step"]: p["psnr"] for p in d["psnr"]}
+    return runs
+
+
+def stats(xs):
+    n = len(xs)
+    m = sum(xs) / n
+    sd = math.sqrt(sum((x - m) ** 2 for x in xs) / (n - 1)) if n > 1 else float("nan")
+    return n, m, sd
+
+
+def t975(df):
+    """two-sided 95% Student-t quantile (table + asymptote)."""
+    table = {1: 12.71, 2: 4.30, 3: 3.18, 4: 2.78, 5: 2.57, 6: 2.45, 7: 2.36, 8: 2.31, 9: 2.26,
+             10: 2.23, 12: 2.18, 15: 2.13, 20: 2.09, 25: 2.06, 30: 2.04, 40: 2.02, 60: 2.00}
+    df = max(1, int(df))
+    for k in sorted(table):
+        if df <= k:
+            return table[k]
+    return 1.96
+
+
+def main():
+    groups = {
+        "f16x3": load("profiles/r03/psnr/f16x3_s*.json"),
+        "fp32": load("profiles/r03/psnr/fp32_s*.json"),
+        "ref_gpu": load("profiles/r03/psnr/oracle_s*.json"),
+        "ref_cpu": load("profiles/r01/psnr_reference_s*.json", "profiles/r02/psnr/reference_s*.json",
+                        "profiles/r03/psnr/reference_s*.json"),
+    }
+    groups["ref_all"] = {("g", s): v for s, v in groups["ref_gpu"].items()}
+    groups["ref_all"].update({("c", s): v for s, v in groups["ref_cpu"].items()})
+    pairs = [("f16x3", "ref_all"), ("fp32", "ref_all"), ("f16x3", "ref_gpu"), ("f16x3", "ref_cpu"),
+             ("fp32", "ref_gpu"), ("f16x3", "fp32"), ("ref_gpu", "ref_cpu")]
+    out = {"groups": {k: sorted(map(str, v)) for k, v in groups.items()}, "checkpoints": []}
+    for step in STEPS:
+        row = {"step": step, "groups": {}, "diffs": {}}
+        vals = {k: [r[step] for r in v.values() if step in r] for k, v in groups.items()}
+        for k, xs in vals.items():
+            if xs:
+                n, m, sd = stats(xs)
+                row["groups"][k] = {"n": n, "mean": round(m, 3),
+                                    "std": None if n < 2 else round(sd, 3)}
+        for a, b in pairs:
+            if len(vals[a]) < 2 or len(vals[b]) < 2:
+                continue
+            na, ma, sa = stats(vals[a])
+            nb, mb, sb = stats(vals[b])
+            va, vb = sa ** 2 / na, sb ** 2 / nb
+            se = math.sqrt(va + vb)
+            df = (va + vb) ** 2 / (va ** 2 / (na - 1) + vb ** 2 / (nb - 1))   # Welch
+            half = t975(df) * se
+            d = ma - mb
+            row["diffs"][f"{a}-{b}"] = {
+                "diff": round(d, 3), "se": round(se, 3), "ci95": [round(d - half, 3), round(d + half, 3)],
+                "ci95_within_0.1dB": bool(abs(d) + half <= 0.1), "n": [na, nb]}
+        out["checkpoints"].append(row)
+        print(json.dumps(row))
+    path = os.path.join(REPO, "profiles", "r03", "psnr", "summary.json")
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()

@@ -10,6 +10,30 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
+
+def _to_np(x):
+    """tensors -> numpy for the result queue: a tensor put on a multiprocessing
+    queue is shared through a file descriptor that vanishes when the worker
+    exits first (a race); numpy arrays are pickled by value"""
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_np(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _to_np(v) for k, v in x.items()}
+    return x
+
+
+def _to_t(x):
+    import numpy as np
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(x)
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_t(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _to_t(v) for k, v in x.items()}
+    return x
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -35,7 +59,7 @@ def _worker(rank, world, port, q):
         loss.backward()
         red = GradAllReducer(list(model.parameters()) + [unused])
         red()
-        q.put((rank, [p.grad.clone() for p in model.parameters()], unused.grad.clone()))
+        q.put(_to_np(((rank, [p.grad.clone() for p in model.parameters()], unused.grad.clone()))))
     finally:
         dist.destroy_process_group()
 
@@ -48,7 +72,7 @@ def test_grad_allreduce_matches_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [_to_t(q.get(timeout=120)) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -90,7 +114,7 @@ def _bucket_worker(rank, world, port, q):
             # numpy: pickled by value (tensors would be shared through file
             # descriptors that die with this process)
             out.append([p.grad.numpy().copy() for p in list(ma.parameters()) + list(mb.parameters())])
-        q.put((rank, out))
+        q.put(_to_np(((rank, out))))
     finally:
         dist.destroy_process_group()
 
@@ -115,7 +139,7 @@ def test_bucketed_allreduce_overlapped_from_hooks():
     procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [_to_t(q.get(timeout=120)) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -129,7 +153,7 @@ def test_bucketed_allreduce_overlapped_from_hooks():
         ref = [p.grad for p in list(ma.parameters()) + list(mb.parameters())]
         for rank, out in res:
             for a, b in zip(out[it], ref):
-                torch.testing.assert_close(torch.from_numpy(a), b, rtol=1e-6, atol=1e-7)
+                torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
 
 
 def _shard_worker(rank, world, port, q, n):
@@ -145,7 +169,7 @@ def _shard_worker(rank, world, port, q, n):
             seen.append((xs.shape[0], tag))
             return {"sum": xs.sum(1), "twice": 2 * xs, "none": None}
         out = sharded_map(fn, x, rank_args=lambda lo, hi: {"tag": (lo, hi)})
-        q.put((rank, out["sum"], out["twice"], out["none"], seen))
+        q.put(_to_np(((rank, out["sum"], out["twice"], out["none"], seen))))
     finally:
         dist.destroy_process_group()
 
@@ -161,7 +185,7 @@ def test_sharded_map_gathers_every_row():
         procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q, n)) for r in range(world)]
         for p in procs:
             p.start()
-        res = [q.get(timeout=120) for _ in range(world)]
+        res = [_to_t(q.get(timeout=120)) for _ in range(world)]
         for p in procs:
             p.join(timeout=60)
             assert p.exitcode == 0
@@ -192,12 +216,12 @@ def _shard_grad_worker(rank, world, port, q, n, mismatch):
         try:
             out = sharded_map(fn, x)
         except RuntimeError as e:
-            q.put((rank, "raised", str(e)))
+            q.put(_to_np(((rank, "raised", str(e)))))
             return
         # rank-dependent loss on the gathered rows (each rank's own camera batch)
         coef = torch.arange(n, dtype=torch.float32) * (rank + 1)
         (out["y"] * coef).sum().backward()
-        q.put((rank, "ok", w.grad.clone()))
+        q.put(_to_np(((rank, "ok", w.grad.clone()))))
     finally:
         dist.destroy_process_group()
 
@@ -209,7 +233,7 @@ def _run(world, target, *args):
     procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted((q.get(timeout=120) for _ in range(world)), key=lambda r: r[0])
+    res = sorted((_to_t(q.get(timeout=120)) for _ in range(world)), key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -257,7 +281,7 @@ def _sampler_worker(rank, world, port, q, total, batch, steps):
         # CPU poses: only the index partitioning is exercised (no ray generation)
         s = RaySampler(torch.zeros(total, 3, 4), 1, 1, 1.0, 2.0, 6.0, seed=7, rank=rank,
                        world=world)
-        q.put((rank, [s.next_indices(batch).clone() for _ in range(steps)], s.epoch))
+        q.put(_to_np(((rank, [s.next_indices(batch).clone() for _ in range(steps)], s.epoch))))
     finally:
         dist.destroy_process_group()
 

@@ -18,6 +18,30 @@ pytestmark = pytest.mark.gpu
 S, I, N = 32, 32, 777
 
 
+
+def _to_np(x):
+    """tensors -> numpy for the result queue: a tensor put on a multiprocessing
+    queue is shared through a file descriptor that vanishes when the worker
+    exits first (a race); numpy arrays are pickled by value"""
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_np(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _to_np(v) for k, v in x.items()}
+    return x
+
+
+def _to_t(x):
+    import numpy as np
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(x)
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_t(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _to_t(v) for k, v in x.items()}
+    return x
+
 def _setup():
     from nerf_pl_amd import Embedding, NeRF
     from nerf_pl_amd.rays import blender_rays
@@ -48,7 +72,7 @@ def _worker(rank, world, port, q):
                 models, emb, rays, S, False, 1.0, 0.0, I, 32768, False,
                 rng_for_rows=lambda lo, hi: ReplayRNG([d[lo:hi] for d in draws]))
         torch.cuda.synchronize()
-        q.put((rank, {k: v.cpu() for k, v in out.items()}))
+        q.put(_to_np(((rank, {k: v.cpu() for k, v in out.items()}))))
     finally:
         dist.destroy_process_group()
 
@@ -71,7 +95,7 @@ def test_sharded_light_render_matches_replicated():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=100) for _ in range(world)]
+    res = [_to_t(q.get(timeout=100)) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -79,3 +103,77 @@ def test_sharded_light_render_matches_replicated():
         assert sorted(out) == sorted(ref)
         for k in ref:
             assert torch.equal(out[k], ref[k]), (rank, k)
+
+
+def _grad_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nerf_pl_amd import ReplayRNG
+        from nerf_pl_amd import rendering_shadows as RS
+        from nerf_pl_amd.distributed import GradAllReducer
+        models, emb, rays, draws = _setup()
+        # --grad_on_light: the sharded light render keeps its graph
+        out = RS.render_rays_sharded(models, emb, rays, S, False, 1.0, 0.0, I, 32768, False,
+                                     rng_for_rows=lambda lo, hi: ReplayRNG([d[lo:hi] for d in draws]))
+        _rank_loss(out, rank).backward()
+        params = [p for m in models for p in m.parameters()]
+        GradAllReducer(params)()
+        torch.cuda.synchronize()
+        q.put(_to_np(((rank, [p.grad.cpu() if p.grad is not None else None for p in params]))))
+    finally:
+        dist.destroy_process_group()
+
+
+def _rank_loss(out, rank):
+    # each rank's own loss on the whole light map (its camera batch, under DDP)
+    g = torch.Generator().manual_seed(100 + rank)
+    loss = 0
+    for k in ("depth_coarse", "depth_fine"):
+        c = torch.randn(out[k].shape, generator=g).to(out[k].device)
+        loss = loss + (out[k] * c).sum()
+    return loss
+
+
+def test_sharded_light_render_gradients_match_replicated():
+    """--grad_on_light with the light image sharded over 2 ranks: after the
+    gather's reduce-scatter backward and the parameter all-reduce, every rank
+    holds the mean over ranks of the gradient each would get rendering the
+    whole light image itself (the reference under DDP)."""
+    from nerf_pl_amd import ReplayRNG
+    from nerf_pl_amd import rendering_shadows as RS
+    world = 2
+    models, emb, rays, draws = _setup()
+    params = [p for m in models for p in m.parameters()]
+    ref = [torch.zeros_like(p) for p in params]
+    for r in range(world):
+        for p in params:
+            p.grad = None
+        out = RS.render_rays(models, emb, rays, S, False, 1.0, 0.0, I, 32768, False,
+                             rng=ReplayRNG(draws))
+        _rank_loss(out, r).backward()
+        for acc, p in zip(ref, params):
+            if p.grad is not None:
+                acc += p.grad / world
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [_to_t(q.get(timeout=100)) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, grads in res:
+        for (name, _), g, e in zip([(n, p) for m in models for n, p in m.named_parameters()],
+                                   grads, ref):
+            e = e.cpu()
+            g = torch.zeros_like(e) if g is None else g
+            scale = e.abs().max().item() + 1e-30
+            torch.testing.assert_close(g, e, rtol=1e-4, atol=1e-5 * scale,
+                                       msg=lambda m: f"rank {rank} {name}: {m}")
