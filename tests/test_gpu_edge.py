@@ -19,6 +19,7 @@ import pytest
 import torch
 
 from oracle import nerf_oracle as O
+from screening import pdf_flips
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -97,6 +98,12 @@ def test_full_batch_matches_oracle(kind):
                         rng=O.ReplayRNG(draws), capture=ocap)
     zf = cap["z_fine"].cpu().numpy()
     bad = np.abs(zf - ocap["z_fine"].numpy()).max(1) > 1e-4 * np.maximum(1, np.abs(zf).max(1))
+    # every screened ray explained: a reference importance depth missing from
+    # ours, its u within 1e-5 of a reference CDF knot (screening.pdf_flips)
+    moved, explained = pdf_flips(cap["z_fine"], ocap, draws[-3])
+    assert not (bad & ~moved).any(), "z_fine differs although every importance depth matches"
+    assert not (moved & ~explained).any(), \
+        f"z_fine moved away from any CDF knot: rays {np.nonzero(moved & ~explained)[0][:8]}"
     assert bad.mean() <= 0.01, f"{bad.sum()} rays with a sample_pdf bin flip"
     assert sorted(res) == sorted(ref)
     _compare(res, ref, bad)

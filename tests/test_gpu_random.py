@@ -25,6 +25,7 @@ import pytest
 import torch
 
 from oracle import nerf_oracle as O
+from screening import pdf_flips
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -92,6 +93,11 @@ def _run(c, grad=False):
     if c["I"] > 0:
         zf, ozf = cap["z_fine"].detach().cpu().numpy(), ocap["z_fine"].detach().numpy()
         bad = np.abs(zf - ozf).max(1) > 1e-4 * np.maximum(1, np.abs(zf).max(1))
+        # every screened ray explained by a u within 1e-5 of a reference CDF knot
+        ocap = {k: v.detach() for k, v in ocap.items()}
+        moved, explained = pdf_flips(cap["z_fine"], ocap, draws[-3])
+        assert not (bad & ~moved).any(), f"z_fine differs without a moved importance depth, {c}"
+        assert not (moved & ~explained).any(), f"z_fine moved away from any CDF knot, {c}"
     return models, params, res, ref, bad
 
 
