@@ -47,9 +47,46 @@ def reference_functions():
     keep = [n for n in tree.body
             if isinstance(n, ast.FunctionDef) and n.name in ("get_rays", "get_ndc_rays")]
     assert len(keep) == 2, "reference ray_utils.py changed"
-    ns = {"torch": torch}
+    _vet(keep)
+    # no builtins: the two bodies may reach torch and their own arguments only
+    ns = {"torch": torch, "__builtins__": {}}
     exec(compile(ast.Module(body=keep, type_ignores=[]), path, "exec"), ns)
     return ns["get_rays"], ns["get_ndc_rays"]
+
+
+_ALLOWED_ATTRS = {"T", "norm", "expand", "shape", "view", "stack", "reshape", "unsqueeze"}
+
+
+def _vet(defs):
+    """The untrusted reference code is executed only after this check (ADVICE
+    r2): plain arithmetic, subscripts and assignments over the function's own
+    names, calls only of torch.<fn> or of whitelisted tensor methods; no
+    decorators, imports, defaults that call, lambdas, comprehensions, loops,
+    with-blocks, attribute access to dunders or globals other than torch."""
+    ok_nodes = (ast.FunctionDef, ast.arguments, ast.arg, ast.Expr, ast.Constant, ast.Assign,
+                ast.Return, ast.Name, ast.Load, ast.Store, ast.BinOp, ast.UnaryOp, ast.Add,
+                ast.Sub, ast.Mult, ast.Div, ast.USub, ast.MatMult, ast.Pow, ast.Subscript,
+                ast.Slice, ast.Tuple, ast.List, ast.Attribute, ast.Call, ast.keyword, ast.Ellipsis
+                if hasattr(ast, "Ellipsis") else ast.Constant)
+    for fn in defs:
+        assert not fn.decorator_list, "decorated reference function"
+        assert all(isinstance(d, ast.Constant) for d in fn.args.defaults), "computed default"
+        local = {a.arg for a in fn.args.args}
+        for node in ast.walk(fn):
+            assert isinstance(node, ok_nodes), f"{fn.name}: {type(node).__name__} not allowed"
+            if isinstance(node, ast.Assign):
+                for t in node.targets:
+                    for n in ast.walk(t):
+                        if isinstance(n, ast.Name):
+                            local.add(n.id)
+            if isinstance(node, ast.Attribute):
+                assert not node.attr.startswith("_"), f"{fn.name}: dunder attribute"
+                base = node.value
+                if isinstance(base, ast.Name) and base.id == "torch":
+                    continue
+                assert node.attr in _ALLOWED_ATTRS, f"{fn.name}: .{node.attr} not allowed"
+            if isinstance(node, ast.Name) and isinstance(node.ctx, ast.Load):
+                assert node.id in local or node.id == "torch", f"{fn.name}: global {node.id}"
 
 
 def poses(k, ndc):
