@@ -71,8 +71,15 @@ BYTES_WGRAD = 4 * (2528 + 2436)                     # 19,856
 # bf16 variant: every segment stored in bf16 except the 4-float head gradient
 # (itself bf16 too: 8 B/sample) -> 2 * (2528 + 2436) = 9,928
 BYTES_WGRAD_BF16 = 2 * (2528 + 2436)
+# the sigma-only graph trained on its own kernels (rendering_shadows.py:167):
+# data gradient without layer 1 and layer 5's PE columns; weight gradient of
+# xyz_encoding_1..8 + sigma, reading PE, h1..h8, dz1..dz8 and the head once
+FLOP_DGRAD_SIGMA = FLOP_FWD_SIGMA - 2 * 2 * 63 * 256             # 918,016
+BYTES_WGRAD_SIGMA = 4 * (64 + 8 * 256 + 8 * 256 + 4)             # 16,656
 KERNEL_FLOP = {"mlp_fwd": FLOP_FWD, "mlp_fwd_sigma": FLOP_FWD_SIGMA,
-               "mlp_bwd_dgrad": FLOP_DGRAD, "mlp_wgrad": FLOP_WGRAD}
+               "mlp_fwd_sigma_train": FLOP_FWD_SIGMA,
+               "mlp_bwd_dgrad": FLOP_DGRAD, "mlp_bwd_dgrad_sigma": FLOP_DGRAD_SIGMA,
+               "mlp_wgrad": FLOP_WGRAD, "mlp_wgrad_sigma": FLOP_FWD_SIGMA}
 CONFIGS = ("cfg2", "cfg3", "cfg4", "cfg5", "eval")
 
 
@@ -100,13 +107,17 @@ def kernel_roofline(k, events, math_, traffic_json):
     # the weight gradient streams every saved segment once at 60 FLOP/B: below
     # the ridge (peak FLOP/s / 8 TB/s) of the split arithmetics, HBM-bound;
     # above the fp32 MFMA ridge (19.7 FLOP/B), MFMA-bound
-    bps = BYTES_WGRAD_BF16 if math_ == "bf16" else BYTES_WGRAD
-    if k == "mlp_wgrad" and flops / bps < peak * 1e12 / (HBM_PEAK_GBS * 1e9):
+    bps = BYTES_WGRAD_SIGMA if k == "mlp_wgrad_sigma" else BYTES_WGRAD
+    if math_ == "bf16":
+        bps //= 2
+    if k.startswith("mlp_wgrad") and flops / bps < peak * 1e12 / (HBM_PEAK_GBS * 1e9):
         ach = bps * nmax / (avg * 1e-3) / 1e9
         return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 4), bytes_per_sample=bps,
-                    bytes_basis="every saved activation (2528 values/sample) and gradient "
-                                "(2436 values/sample) segment read once, "
+                    bytes_basis=("every saved activation (2528 values/sample) and gradient "
+                                 "(2436 values/sample) segment read once, " if k == "mlp_wgrad"
+                                 else "the sigma-only graph's saved PE, h1..h8, dz1..dz8 and "
+                                      "head (4164 values/sample) read once, ")
                                 + ("bf16" if math_ == "bf16" else "fp32"),
                     tflops_fp32_equiv=round(tflops, 2), **common)
     basis = {
@@ -201,11 +212,17 @@ def install_timers(timer):
     def call_tag(name, *a):
         base = name[:-3] if name[-3:] in ("_x3", "_h3", "_b1") else name
         if base == "nr_mlp_fwd":
-            return ("mlp_fwd_sigma" if a[7] else "mlp_fwd"), int(a[3])
+            if a[7]:     # sigma_only: inference, or the sigma-only training forward (save)
+                return ("mlp_fwd_sigma_train" if a[9] else "mlp_fwd_sigma"), int(a[3])
+            return "mlp_fwd", int(a[3])
         if base == "nr_mlp_bwd":
             return "mlp_bwd_dgrad", int(a[5])
+        if base == "nr_mlp_bwd_sigma":
+            return "mlp_bwd_dgrad_sigma", int(a[5])
         if base == "nr_wgrad":
             return "mlp_wgrad", int(a[2])
+        if base == "nr_wgrad_sigma":
+            return "mlp_wgrad_sigma", int(a[2])
         if name == "nr_adam_step":
             return "adam", 0
         return name[3:], 0

@@ -131,6 +131,32 @@ int nr_mlp_bwd_b1(const void* packed_bwd, const float* head, const float* out, c
 int nr_wgrad_b1(const float* save, const float* grad_ws, int64_t n, float* workspace,
                 float* grad_flat, void* stream);
 
+/* Training the sigma-only graph (models/rendering_shadows.py:167: every MLP
+ * call of the shadow path is NeRF.forward(x, sigma_only=True)) on the split
+ * arithmetics: nr_mlp_fwd_{x3,h3,b1} with sigma_only = 1 AND a save buffer
+ * (ray path) runs layers 1-8 and the sigma head only, keeps the activations
+ * those layers need and writes (n, 4) rows [0, 0, 0, sigma];
+ * nr_mlp_bwd_sigma_* (g_out column 3 = d sigma, the rgb columns ignored)
+ * starts the data-gradient chain at d h8 = W_sigma^T d sigma; nr_wgrad_sigma_*
+ * computes the weight gradients of xyz_encoding_1..8 and the sigma head and
+ * writes 0 for xyz_encoding_final, dir_encoding and rgb (not in the graph).
+ * Contracts otherwise those of nr_mlp_bwd_* / nr_wgrad_*. */
+int nr_mlp_bwd_sigma_x3(const void* packed_bwd, const float* head, const float* out,
+                        const float* g_out, const float* save, int64_t n, float* grad_ws,
+                        void* stream);
+int nr_mlp_bwd_sigma_h3(const void* packed_bwd, const float* head, const float* out,
+                        const float* g_out, const float* save, int64_t n, float* grad_ws,
+                        void* stream);
+int nr_mlp_bwd_sigma_b1(const void* packed_bwd, const float* head, const float* out,
+                        const float* g_out, const float* save, int64_t n, float* grad_ws,
+                        void* stream);
+int nr_wgrad_sigma_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                      float* grad_flat, void* stream);
+int nr_wgrad_sigma_h3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                      float* grad_flat, void* stream);
+int nr_wgrad_sigma_b1(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                      float* grad_flat, void* stream);
+
 /* Dense sigma query (extract_color_mesh.py:114-137, the marching-cubes grid):
  * sigma_out (n) = NeRF sigma head at points pts (n,3) -- the sigma-only fused
  * kernel with the positional encoding computed in-kernel (sigma does not

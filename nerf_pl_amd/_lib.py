@@ -30,21 +30,27 @@ SIGNATURES = {
     "nr_mlp_sigma_points_x3": [_p, _p, _i64, _p, _p],
     "nr_pack_bwd_x3": [_p, _p, _i64, _p, _p],
     "nr_mlp_bwd_x3": [_p, _p, _p, _p, _p, _i64, _p, _p],
+    "nr_mlp_bwd_sigma_x3": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_x3": [_p, _p, _i64, _p, _p, _p],
+    "nr_wgrad_sigma_x3": [_p, _p, _i64, _p, _p, _p],
     "nr_fwd3_packed_bytes_h3": [],
     "nr_pack_h3": [_p, _p, _i64, _p, _p, _p],
     "nr_mlp_fwd_h3": [_p, _p, _p, _i64, _i, _p, _i, _i, _p, _p, _p],
     "nr_mlp_sigma_points_h3": [_p, _p, _i64, _p, _p],
     "nr_pack_bwd_h3": [_p, _p, _i64, _p, _p],
     "nr_mlp_bwd_h3": [_p, _p, _p, _p, _p, _i64, _p, _p],
+    "nr_mlp_bwd_sigma_h3": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_h3": [_p, _p, _i64, _p, _p, _p],
+    "nr_wgrad_sigma_h3": [_p, _p, _i64, _p, _p, _p],
     "nr_fwd3_packed_bytes_b1": [],
     "nr_pack_b1": [_p, _p, _i64, _p, _p, _p],
     "nr_mlp_fwd_b1": [_p, _p, _p, _i64, _i, _p, _i, _i, _p, _p, _p],
     "nr_mlp_sigma_points_b1": [_p, _p, _i64, _p, _p],
     "nr_pack_bwd_b1": [_p, _p, _i64, _p, _p],
     "nr_mlp_bwd_b1": [_p, _p, _p, _p, _p, _i64, _p, _p],
+    "nr_mlp_bwd_sigma_b1": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_b1": [_p, _p, _i64, _p, _p, _p],
+    "nr_wgrad_sigma_b1": [_p, _p, _i64, _p, _p, _p],
     "nr_mlp_bwd": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
     "nr_sm_workspace_bytes": [_i64, _i64],

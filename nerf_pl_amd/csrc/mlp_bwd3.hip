@@ -153,7 +153,14 @@ struct Bwd3Args {
     float* stats;    // f16x3: per-wave maxima [NR_STAT_SEGS][nb] (layout.h, in the save buffer)
 };
 
+// SO: the sigma-only graph (rendering_shadows.py:167, sigma_only=True): no rgb
+// head, dir layer or xyz_encoding_final, so the chain starts at d h8 =
+// W_sigma^T dsigma and the ring streams the transposed weights from layer 8
+// on (the packed buffer from group kL8T, the group indices shifted by kB)
+template <bool SO>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
+    constexpr int kB = SO ? kL8T : 0;      // first k-group streamed
+    constexpr int QE = kQ - kB;            // groups streamed
     __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -186,8 +193,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 hr, (__attribute__((address_space(3))) void*)(Hs + i * 256), 16, lane * 16, i * 1024, 0, 0);
     }
-    const Dma dma = make_dma(PB, BwdTab::off(kQ), smem, wave, lane);
-    prologue<BwdTab, kQ>(dma);
+    const Dma dma = make_dma(PB + BwdTab::off(kB), BwdTab::off(QE), smem, wave, lane);
+    prologue<BwdTab, QE>(dma);
     f32x4 go[2], yo[2];
     bool valid[2];
 #pragma unroll
@@ -203,14 +210,14 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     const uint4* mask = smask + lane;                   // [layer * 64]
     const float* H = Hs;
     Frag f0;                                            // tile-0 fragments of the next k-group
-    enter<BwdTab, 0, kQ>(smem, lane, f0);
+    enter<BwdTab, 0, QE>(smem, lane, f0);
 
     float dzr[2][3], dsig[2];
 #pragma unroll
     for (int S = 0; S < 2; ++S) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-            dzr[S][c] = valid[S] ? go[S][c] * (1.f - yo[S][c]) * yo[S][c] : 0.f;
+        for (int c = 0; c < 3; ++c)   // (the sigma-only graph has no rgb output)
+            dzr[S][c] = valid[S] && !SO ? go[S][c] * (1.f - yo[S][c]) * yo[S][c] : 0.f;
         dsig[S] = valid[S] ? go[S][3] : 0.f;
     }
     if (live && g < 2) {     // lane group g < 2 writes sample tile S = g
@@ -233,27 +240,6 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         report_max(m, a.stats + 10 * nb + blk, lane);
     }
 
-    // d hdir = W_rgb^T dz_rgb, masked by the dir-layer ReLU -> dz_dir (128)
-    f32x4 C[8][2];
-    {
-        const uint4 mk = mask[8 * 64];
-        const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
-#pragma unroll
-        for (int F = 0; F < 8; ++F) {
-            const int f = 16 * F + 4 * g;
-            const f32x4 w0 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + f);
-            const f32x4 w1 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 128 + f);
-            const f32x4 w2 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 256 + f);
-#pragma unroll
-            for (int S = 0; S < 2; ++S)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float d = fmaf(w2[r], dzr[S][2], fmaf(w1[r], dzr[S][1], w0[r] * dzr[S][0]));
-                    C[F][S][r] = mask_keep(d, mw, F, S, r);
-                }
-        }
-    }
-
     Act A, B;
     Pieces b[2];
     NoSide none;
@@ -269,75 +255,127 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     GradU<16, true> NAME{X, dzseg(DZ), {0u, 0u, 0u, 0u}, lane};     \
     mwords(ML, NAME.mw);
 
-    // d feat = W_dir[:, :256]^T dz_dir (xyz_encoding_final has no activation); stores dz_dir
-    GradU<8, false> uc{C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_SEGF(128), {0u, 0u, 0u, 0u},
-                       lane};
-    GradU<16, false> ua{A, dzseg(8), {0u, 0u, 0u, 0u}, lane};     // dfeat
-    // f16x3: the sigma head injects w_sigma dsigma (|.| <= max|w_sigma| |dsigma|)
-    // into d h8.  The scales of dz_dir's and dfeat's B values are bounded by it
-    // too, so the d h8 accumulator (which inherits dfeat's scale) stays finite
-    // when dsigma dwarfs the rgb gradient (the 1e10 last-sample delta).
-    float inj[2] = {0.f, 0.f};   // max|w_sigma| |dsigma|, true units
-    if constexpr (NR_F16) {
-        float wm = 0.f;
-#pragma unroll
-        for (int F = 0; F < 16; ++F) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(H + NR_H_WSIG + 16 * F + 4 * g);
-            wm = fmaxf(wm, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
-        }
-        wm = max_over_groups(wm);
-#pragma unroll
-        for (int S = 0; S < 2; ++S) {
-            inj[S] = wm * fabsf(dsig[S]);
-            // dz_dir holds true values: its B scale from its own max (and the injection)
-            float m = 0.f;
-#pragma unroll
-            for (int F = 0; F < 8; ++F)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(C[F][S][r]));
-            const float f = pow2_norm(fmaxf(max_over_groups(m), inj[S]), kGT, kGLim);
-            uc.sc.ks[S] = f;
-            uc.sc.sig[S] = f;
-            ua.inj[S] = inj[S] * f;
-        }
-    }
-    split_all(uc, b);
-    segment<BwdTab, kDirT, 4, 2, kQ, true>(dma, lane, A, uc, ua, zero, none, b, f0);
-    uc.report(STW + 9 * nb);
-    // d h8 = W_final^T dfeat + W_sigma^T dsigma; dz8 = d h8 * [h8 > 0]
     NR_GRADU(u8, B, 7, 7)
-    if constexpr (NR_F16) {
+    if constexpr (!SO) {
+        // d hdir = W_rgb^T dz_rgb, masked by the dir-layer ReLU -> dz_dir (128)
+        f32x4 C[8][2];
+        {
+            const uint4 mk = mask[8 * 64];
+            const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
 #pragma unroll
-        for (int S = 0; S < 2; ++S) u8.inj[S] = inj[S] * ua.sc.sig[S];   // in dfeat's B units
+            for (int F = 0; F < 8; ++F) {
+                const int f = 16 * F + 4 * g;
+                const f32x4 w0 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + f);
+                const f32x4 w1 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 128 + f);
+                const f32x4 w2 = *reinterpret_cast<const f32x4*>(H + NR_H_WRGB + 256 + f);
+#pragma unroll
+                for (int S = 0; S < 2; ++S)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float d = fmaf(w2[r], dzr[S][2], fmaf(w1[r], dzr[S][1], w0[r] * dzr[S][0]));
+                        C[F][S][r] = mask_keep(d, mw, F, S, r);
+                    }
+            }
+        }
+
+        // d feat = W_dir[:, :256]^T dz_dir (xyz_encoding_final has no activation); stores dz_dir
+        GradU<8, false> uc{C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_SEGF(128), {0u, 0u, 0u, 0u},
+                           lane};
+        GradU<16, false> ua{A, dzseg(8), {0u, 0u, 0u, 0u}, lane};     // dfeat
+        // f16x3: the sigma head injects w_sigma dsigma (|.| <= max|w_sigma| |dsigma|)
+        // into d h8.  The scales of dz_dir's and dfeat's B values are bounded by it
+        // too, so the d h8 accumulator (which inherits dfeat's scale) stays finite
+        // when dsigma dwarfs the rgb gradient (the 1e10 last-sample delta).
+        float inj[2] = {0.f, 0.f};   // max|w_sigma| |dsigma|, true units
+        if constexpr (NR_F16) {
+            float wm = 0.f;
+#pragma unroll
+            for (int F = 0; F < 16; ++F) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(H + NR_H_WSIG + 16 * F + 4 * g);
+                wm = fmaxf(wm, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+            }
+            wm = max_over_groups(wm);
+#pragma unroll
+            for (int S = 0; S < 2; ++S) {
+                inj[S] = wm * fabsf(dsig[S]);
+                // dz_dir holds true values: its B scale from its own max (and the injection)
+                float m = 0.f;
+#pragma unroll
+                for (int F = 0; F < 8; ++F)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(C[F][S][r]));
+                const float f = pow2_norm(fmaxf(max_over_groups(m), inj[S]), kGT, kGLim);
+                uc.sc.ks[S] = f;
+                uc.sc.sig[S] = f;
+                ua.inj[S] = inj[S] * f;
+            }
+        }
+        split_all(uc, b);
+        segment<BwdTab, kDirT - kB, 4, 2, QE, true>(dma, lane, A, uc, ua, zero, none, b, f0);
+        uc.report(STW + 9 * nb);
+        // d h8 = W_final^T dfeat + W_sigma^T dsigma; dz8 = d h8 * [h8 > 0]
+        if constexpr (NR_F16) {
+#pragma unroll
+            for (int S = 0; S < 2; ++S) u8.inj[S] = inj[S] * ua.sc.sig[S];   // in dfeat's B units
+        }
+        {
+            // the accumulator carries 2^kWScale sigma(dfeat) (f16x3), so does its C operand
+            // (dsigma * sigma first: 2^kWScale * sigma alone may overflow when dsigma is 0)
+            constexpr float kW = (float)(1 << kWScale);
+            SigInit si{H + NR_H_WSIG, g, NR_F16 ? dsig[0] * ua.sc.sig[0] * kW : dsig[0],
+                       NR_F16 ? dsig[1] * ua.sc.sig[1] * kW : dsig[1]};
+            segment<BwdTab, kFinalT - kB, 8, 2, QE, true>(dma, lane, B, ua, u8, si, none, b, f0);
+        }
+        ua.report(STW + 8 * nb);
+    } else {
+        // d h8 = W_sigma^T dsigma (nerf.py:112), the accumulator filled directly
+        // in the units the full graph's xyz_encoding_final segment leaves it in
+        // (2^kWScale x the producer's scale, here a unit-scale virtual producer)
+        float inj[2] = {0.f, 0.f};
+        if constexpr (NR_F16) {
+            float wm = 0.f;
+#pragma unroll
+            for (int F = 0; F < 16; ++F) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(H + NR_H_WSIG + 16 * F + 4 * g);
+                wm = fmaxf(wm, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+            }
+            wm = max_over_groups(wm);
+#pragma unroll
+            for (int S = 0; S < 2; ++S) u8.inj[S] = inj[S] = wm * fabsf(dsig[S]);
+        }
+        constexpr float kW = NR_F16 ? (float)(1 << kWScale) : 1.f;
+        const SigInit si{H + NR_H_WSIG, g, dsig[0] * kW, dsig[1] * kW};
+#pragma unroll
+        for (int F = 0; F < 16; ++F)
+#pragma unroll
+            for (int S = 0; S < 2; ++S) B[F][S] = si(F, S);
+        struct { GScale sc; } unit;
+        u8.begin(unit);
+        split_all(u8, b);
+        if constexpr (NR_F16) {     // dfeat and dz_dir are not part of this graph
+            report_max(0.f, STW + 8 * nb, lane);
+            report_max(0.f, STW + 9 * nb, lane);
+        }
     }
-    {
-        // the accumulator carries 2^kWScale sigma(dfeat) (f16x3), so does its C operand
-        // (dsigma * sigma first: 2^kWScale * sigma alone may overflow when dsigma is 0)
-        constexpr float kW = (float)(1 << kWScale);
-        SigInit si{H + NR_H_WSIG, g, NR_F16 ? dsig[0] * ua.sc.sig[0] * kW : dsig[0],
-                   NR_F16 ? dsig[1] * ua.sc.sig[1] * kW : dsig[1]};
-        segment<BwdTab, kFinalT, 8, 2, kQ, true>(dma, lane, B, ua, u8, si, none, b, f0);
-    }
-    ua.report(STW + 8 * nb);
     NR_GRADU(u7, A, 6, 6)
-    segment<BwdTab, kL8T, 8, 2, kQ, true>(dma, lane, A, u8, u7, zero, none, b, f0);
+    segment<BwdTab, kL8T - kB, 8, 2, QE, true>(dma, lane, A, u8, u7, zero, none, b, f0);
     u8.report(STW + 7 * nb);
     NR_GRADU(u6, B, 5, 5)
-    segment<BwdTab, kL7T, 8, 2, kQ, true>(dma, lane, B, u7, u6, zero, none, b, f0);
+    segment<BwdTab, kL7T - kB, 8, 2, QE, true>(dma, lane, B, u7, u6, zero, none, b, f0);
     u7.report(STW + 6 * nb);
     NR_GRADU(u5, A, 4, 4)
-    segment<BwdTab, kL6T, 8, 2, kQ, true>(dma, lane, A, u6, u5, zero, none, b, f0);
+    segment<BwdTab, kL6T - kB, 8, 2, QE, true>(dma, lane, A, u6, u5, zero, none, b, f0);
     u6.report(STW + 5 * nb);
     NR_GRADU(u4, B, 3, 3)   // through the h4 columns of the skip layer
-    segment<BwdTab, kL5T, 8, 2, kQ, true>(dma, lane, B, u5, u4, zero, none, b, f0);
+    segment<BwdTab, kL5T - kB, 8, 2, QE, true>(dma, lane, B, u5, u4, zero, none, b, f0);
     u5.report(STW + 4 * nb);
     NR_GRADU(u3, A, 2, 2)
-    segment<BwdTab, kL4T, 8, 2, kQ, true>(dma, lane, A, u4, u3, zero, none, b, f0);
+    segment<BwdTab, kL4T - kB, 8, 2, QE, true>(dma, lane, A, u4, u3, zero, none, b, f0);
     u4.report(STW + 3 * nb);
     NR_GRADU(u2, B, 1, 1)
-    segment<BwdTab, kL3T, 8, 2, kQ, true>(dma, lane, B, u3, u2, zero, none, b, f0);
+    segment<BwdTab, kL3T - kB, 8, 2, QE, true>(dma, lane, B, u3, u2, zero, none, b, f0);
     u3.report(STW + 2 * nb);
-    segment<BwdTab, kL2T, 8, 2, kQ, true>(dma, lane, A, u2, nonext, zero, none, b, f0);
+    segment<BwdTab, kL2T - kB, 8, 2, QE, true>(dma, lane, A, u2, nonext, zero, none, b, f0);
     u2.report(STW + 1 * nb);
 #undef NR_GRADU
     {   // dz1 = (W2^T dz2) * [h1 > 0]
@@ -404,21 +442,39 @@ NR_API int NR_X3_NAME(nr_pack_bwd)(const float* flat, const int32_t* map, int64_
     return 0;
 }
 
-NR_API int NR_X3_NAME(nr_mlp_bwd)(const void* packed_bwd, const float* head, const float* out,
-                         const float* g_out, const float* save, int64_t n, float* grad_ws,
-                         void* stream) {
-    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_bwd_x3: n out of range");
+namespace {
+int bwd3_launch(const char* name, bool sigma_only, const void* packed_bwd, const float* head,
+                const float* out, const float* g_out, const float* save, int64_t n,
+                float* grad_ws, void* stream) {
+    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "%s: n out of range", name);
     if (n == 0) return 0;
-    NR_REQUIRE(packed_bwd && head && out && g_out && save && grad_ws,
-               "nr_mlp_bwd_x3: null pointer");
+    NR_REQUIRE(packed_bwd && head && out && g_out && save && grad_ws, "%s: null pointer", name);
     NR_REQUIRE((((uintptr_t)save | (uintptr_t)grad_ws | (uintptr_t)g_out | (uintptr_t)out |
                  (uintptr_t)packed_bwd | (uintptr_t)head) & 15) == 0,
-               "nr_mlp_bwd_x3: buffers must be 16-byte aligned");
+               "%s: buffers must be 16-byte aligned", name);
     float* stats = const_cast<float*>(save) + nr_sv_stats(nr_blocks_pad(n)) + NR_STATS;
     Bwd3Args a{reinterpret_cast<const char*>(packed_bwd), head, out, g_out, save, (int)n, grad_ws,
                stats};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
-    mlp_bwd3_kernel<<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
-    NR_LAUNCH_CHECK("nr_mlp_bwd_x3");
+    if (sigma_only) mlp_bwd3_kernel<true><<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
+    else mlp_bwd3_kernel<false><<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
+    NR_LAUNCH_CHECK(name);
     return 0;
+}
+}  // namespace
+
+NR_API int NR_X3_NAME(nr_mlp_bwd)(const void* packed_bwd, const float* head, const float* out,
+                         const float* g_out, const float* save, int64_t n, float* grad_ws,
+                         void* stream) {
+    return bwd3_launch("nr_mlp_bwd_x3", false, packed_bwd, head, out, g_out, save, n, grad_ws,
+                       stream);
+}
+
+// the sigma-only graph's data gradient (g_out column 3 = d sigma; the rgb
+// columns are ignored): save from the sigma-only training forward
+NR_API int NR_X3_NAME(nr_mlp_bwd_sigma)(const void* packed_bwd, const float* head,
+                               const float* out, const float* g_out, const float* save,
+                               int64_t n, float* grad_ws, void* stream) {
+    return bwd3_launch("nr_mlp_bwd_sigma_x3", true, packed_bwd, head, out, g_out, save, n,
+                       grad_ws, stream);
 }

@@ -258,6 +258,22 @@ struct PeU {
 #define NR_STAMP(i) ((void)0)
 #endif
 
+// run a getter over every B unit of the 8 k-steps of a 256-wide activation
+// (its stores as side effect) when no layer consumes it
+template <int S = 0, typename GetU>
+__device__ __forceinline__ void drain_all(GetU& u) {
+    if constexpr (S < 8) {
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                float x0, x1;
+                u(IC<S>(), sb, p, x0, x1);
+            }
+        drain_all<S + 1>(u);
+    }
+}
+
 template <int MODE, bool SIGMA_ONLY, bool SAVE>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     constexpr bool EMB = MODE == FWD_EMB;
@@ -406,7 +422,26 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     const int Sw = g & 1;
     const bool wr = g < 2 && valid[Sw];
     const int sw = smp[Sw];
-    if constexpr (SIGMA_ONLY) {
+    if constexpr (SIGMA_ONLY && SAVE) {
+        // training a sigma-only graph (rendering_shadows.py:167, the shadow
+        // path's every MLP call): layers 1-8 and the sigma head only.  h8 and
+        // its ReLU mask are saved exactly as the full graph saves them while
+        // splitting h8 for xyz_encoding_final, and sigma comes from the same
+        // sums; out rows are (n, 4) [0, 0, 0, sigma] for the backward's contract
+        { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, nonext, bi, none, b, f0); }
+        AccU<true, true, true, true> u8{B, hseg(7), mseg(7), H + NR_H_WSIG, lane, g};
+        drain_all(u8);
+        float sigma[2];
+#pragma unroll
+        for (int S = 0; S < 2; ++S) {
+            float p = u8.sig[S];
+            p += __shfl_xor(p, 16);
+            p += __shfl_xor(p, 32);
+            sigma[S] = p + H[NR_H_BSIG];
+        }
+        if (wr) *reinterpret_cast<f32x4*>(a.out + (size_t)sw * 4) = f32x4{0.f, 0.f, 0.f, Sw ? sigma[1] : sigma[0]};
+        return;
+    } else if constexpr (SIGMA_ONLY) {
         { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, nonext, bi, none, b, f0); }
         float sigma[2];
         head_dot<true>(B, H + NR_H_WSIG, g, sigma);
@@ -560,7 +595,8 @@ NR_API int NR_X3_NAME(nr_mlp_fwd)(const void* packed, const float* rays, const f
     } else {
         NR_REQUIRE(rays && z && samples_per_ray > 0, "nr_mlp_fwd_x3: rays/z/samples_per_ray");
     }
-    NR_REQUIRE(!(sigma_only && save), "nr_mlp_fwd_x3: sigma_only runs keep no activations");
+    NR_REQUIRE(!(sigma_only && save && emb),
+               "nr_mlp_fwd_x3: a sigma_only run keeps activations only on the ray path");
     Fwd3Args a{reinterpret_cast<const char*>(packed), nullptr, rays, z, x, (int)n,
                samples_per_ray, xstride, out, save};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
@@ -572,7 +608,9 @@ NR_API int NR_X3_NAME(nr_mlp_fwd)(const void* packed, const float* rays, const f
         else if (sv) mlp_fwd3_kernel<FWD_EMB, false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
         else mlp_fwd3_kernel<FWD_EMB, false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
     } else {
-        if (sigma_only) mlp_fwd3_kernel<FWD_RAYS, true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+        // sigma_only with save: the sigma-only training forward (out (n, 4))
+        if (sigma_only && sv) mlp_fwd3_kernel<FWD_RAYS, true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else if (sigma_only) mlp_fwd3_kernel<FWD_RAYS, true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
         else if (sv) mlp_fwd3_kernel<FWD_RAYS, false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
         else mlp_fwd3_kernel<FWD_RAYS, false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
     }

@@ -1175,10 +1175,11 @@ NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
 #endif
 
 namespace {
-int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, float* workspace,
-                 float* grad_flat, void* stream) {
-    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_wgrad: n out of range");
-    NR_REQUIRE(save && grad_ws && workspace && grad_flat, "nr_wgrad: null pointer");
+int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_ws, int64_t n,
+                 float* workspace, float* grad_flat, void* stream) {
+    const char* name = sigma_only ? "nr_wgrad_sigma" : "nr_wgrad";
+    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "%s: n out of range", name);
+    NR_REQUIRE(save && grad_ws && workspace && grad_flat, "%s: null pointer", name);
     NR_REQUIRE((((uintptr_t)save | (uintptr_t)grad_ws) & 15) == 0,
                "nr_wgrad: save/grad_ws must be 16-byte aligned");
     hipStream_t st = (hipStream_t)stream;
@@ -1233,8 +1234,13 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     // (the kernel code is unchanged; gradients of the other tasks are then stale)
     // gradient operand's stats slot (layout.h NR_STATS) of every task id
     static const int kStat[kTasks] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 8, 9, 9, 10, 10};
-    static const long long tmask =
+    static const long long tmask_env =
         getenv("NR_WGRAD_TASKMASK") ? strtoll(getenv("NR_WGRAD_TASKMASK"), nullptr, 0) : -1;
+    // the sigma-only graph (rendering_shadows.py:167) has no xyz_encoding_final
+    // (task 9), dir_encoding (10, 11) or rgb head (13): their gradients are not
+    // computed (written as 0; the autograd leaves them None)
+    const long long tmask = sigma_only ? (tmask_env & ~((1LL << 9) | (1LL << 10) | (1LL << 11) | (1LL << 13)))
+                                       : tmask_env;
     int64_t gt[kTasks];
     int pos[kTasks];
     for (int k = 0; k < kTasks; ++k) {
@@ -1257,10 +1263,11 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
     int partner[kTasks];
     bool absorbed[kTasks];
     for (int t = 0; t < kTasks; ++t) { partner[t] = -1; absorbed[t] = false; }
-    if (kFuse && x3 && fuse_on && tmask == -1) {
+    if (kFuse && x3 && fuse_on && (tmask_env == -1)) {
         for (int i = 0; i < 3; ++i) {
             if (!((NR_WGRAD_FUSE_MASK >> i) & 1)) continue;
             const auto& pr = kFused[i];
+            if (!((tmask >> pr[0]) & 1) || !((tmask >> pr[1]) & 1)) continue;   // both must run
             gt[pr[1]] = gt[pr[0]] = std::max<int64_t>(1, std::min<int64_t>(
                 (kTargetWG * (cost[pr[0]] + cost[pr[1]]) + tot - 1) / tot, nb));
             partner[pr[0]] = pr[1];
@@ -1305,11 +1312,18 @@ int wgrad_launch(bool x3, const float* save, const float* grad_ws, int64_t n, fl
 #if NR_X3_BASE_OBJECT
 NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
                     float* grad_flat, void* stream) {
-    return wgrad_launch(false, save, grad_ws, n, workspace, grad_flat, stream);
+    return wgrad_launch(false, false, save, grad_ws, n, workspace, grad_flat, stream);
 }
 #endif
 
 NR_API int NR_X3_NAME(nr_wgrad)(const float* save, const float* grad_ws, int64_t n, float* workspace,
                        float* grad_flat, void* stream) {
-    return wgrad_launch(true, save, grad_ws, n, workspace, grad_flat, stream);
+    return wgrad_launch(true, false, save, grad_ws, n, workspace, grad_flat, stream);
+}
+
+// the sigma-only graph's weight gradients (after nr_mlp_bwd_sigma*): every
+// layer up to xyz_encoding_8 and the sigma head; the other parameters get 0
+NR_API int NR_X3_NAME(nr_wgrad_sigma)(const float* save, const float* grad_ws, int64_t n,
+                             float* workspace, float* grad_flat, void* stream) {
+    return wgrad_launch(true, true, save, grad_ws, n, workspace, grad_flat, stream);
 }

@@ -34,6 +34,10 @@ def _wgrad_workspace(device_index: int, stream: int = 0) -> torch.Tensor:
     return torch.empty(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", device_index))
 
 
+# sigma-only graphs train on the sigma-only kernels (NERF_PL_AMD_SIGMA_TRAIN=0:
+# on the full kernels with a zero rgb gradient -- the A/B reference of the tests)
+SIGMA_TRAIN_KERNELS = os.environ.get("NERF_PL_AMD_SIGMA_TRAIN", "1") != "0"
+
 # NERF_PL_AMD_DEBUG=1 keeps the last backward's buffers here (dev/ scripts)
 _DEBUG = {} if os.environ.get("NERF_PL_AMD_DEBUG") == "1" else None
 
@@ -52,14 +56,20 @@ class _FusedMLP(torch.autograd.Function):
             raise NotImplementedError("nerf_pl_amd: training NeRF.forward(x, sigma_only=True) on "
                                       "pre-embedded input is not supported; use render_rays")
         packed_f, packed_b = model.packed(backward=train)
-        # a sigma-only graph is trained through the full kernel (rgb gradient 0)
-        kern_sigma_only = sigma_only and not train
+        # a sigma-only graph (rendering_shadows.py:167) trains through the
+        # sigma-only training kernels of the split arithmetics (layers 1-8 and
+        # the sigma head: no xyz_encoding_final / dir / rgb work),
+        # through the full kernels with a zero rgb gradient otherwise (fp32)
+        so_train = (train and sigma_only and SIGMA_TRAIN_KERNELS and x is None
+                    and ops.arith_of(packed_f) != "fp32")
+        kern_sigma_only = sigma_only and (not train or so_train)
         out, save = ops.mlp_forward(packed_f, rays=rays, z=z, samples_per_ray=spr, x=x,
                                     sigma_only=kern_sigma_only, save=train)
         if train:
             ctx.save_for_backward(out, save, packed_f, packed_b)
             ctx.sigma_only = sigma_only
-        if sigma_only and not kern_sigma_only:
+            ctx.so_kernels = so_train
+        if sigma_only and train:
             out = out[:, 3:4].contiguous()
         return out
 
@@ -74,11 +84,13 @@ class _FusedMLP(torch.autograd.Function):
             g_out = g4
         grad_ws = torch.empty(ops.n_blocks(n) * ops.GRAD_PER_BLOCK, device=dev)
         g_out = g_out.contiguous()
-        call(ops.entry("nr_mlp_bwd", packed_b), packed_b.data_ptr(), ops.head_ptr(packed_f), out.data_ptr(),
-             g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), stream_of(dev))
+        sfx = "_sigma" if ctx.so_kernels else ""
+        call(ops.entry("nr_mlp_bwd" + sfx, packed_b), packed_b.data_ptr(), ops.head_ptr(packed_f),
+             out.data_ptr(), g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(),
+             stream_of(dev))
         gflat = torch.empty(packing.N_PARAMS, device=dev)
         ws = _wgrad_workspace(dev.index, int(stream_of(dev)))
-        call(ops.entry("nr_wgrad", packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
+        call(ops.entry("nr_wgrad" + sfx, packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
              ws.data_ptr(), gflat.data_ptr(), stream_of(dev))
         if _DEBUG is not None:
             _DEBUG.update(save=save, grad_ws=grad_ws, g_out=g_out, gflat=gflat, n=n)

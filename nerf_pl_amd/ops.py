@@ -190,7 +190,8 @@ def mlp_forward(packed: torch.Tensor, *, rays=None, z=None, samples_per_ray=0, x
         z = _dev(z, "z")
         n, xstride = z.numel(), 0
     dev = packed.device
-    out = torch.empty(n, 1 if sigma_only else 4, device=dev)
+    # a sigma-only training run (save) writes (n, 4) rows [0, 0, 0, sigma]
+    out = torch.empty(n, 1 if sigma_only and not save else 4, device=dev)
     sv = torch.empty(save_floats(n), device=dev) if save else None
     call(entry("nr_mlp_fwd", packed), ptr(packed), ptr(rays), ptr(z), n, int(samples_per_ray),
          ptr(x), xstride, int(sigma_only), ptr(out), ptr(sv), stream_of(dev))

@@ -28,6 +28,12 @@ def _cases():
             (f"nr_wgrad{sfx}", [N, N, 5, N, N, N], NR_EINVAL),
         ]
         if sfx:
+            c += [(f"nr_mlp_bwd_sigma{sfx}", [N, N, N, N, N, -1, N, N], NR_EINVAL),
+                  (f"nr_mlp_bwd_sigma{sfx}", [N, N, N, N, N, 0, N, N], 0),
+                  (f"nr_mlp_bwd_sigma{sfx}", [N, N, N, N, N, 5, N, N], NR_EINVAL),
+                  (f"nr_wgrad_sigma{sfx}", [N, N, -1, N, N, N], NR_EINVAL),
+                  (f"nr_wgrad_sigma{sfx}", [N, N, 5, N, N, N], NR_EINVAL)]
+        if sfx:
             c += [(f"nr_pack{sfx}", [N, N, -1, N, N, N], NR_EINVAL),
                   (f"nr_pack_bwd{sfx}", [N, N, -1, N, N], NR_EINVAL)]
     c += [
