@@ -25,8 +25,9 @@ distance of the reference's fp32 gradient from the same step evaluated in
 float64 by the oracle (``*_bound64``: the fp32 noise floor the GPU test bounds
 its own deviation by, as tests/test_gpu_random.py does).
 
-The cfg5-shaped cases (``cfg5_*``: a 64x64 light image, 512 camera rays, 64 +
-64 samples, light 64 + 64, noise_std 0 as every reference launcher) hold too
+The cfg5-shaped cases (``cfg5_*``: a 64x64 light image -- 128x128 for
+``cfg5_128_sm2``, BASELINE configs[4] exactly -- 512 camera rays, 64 + 64
+samples, light 64 + 64, noise_std 0 as every reference launcher) hold too
 many random draws to commit; they store each draw's kind, shape and checksum
 and the test re-draws them from the recorded seed with the CPU generator
 (``draws_seed``), checking the checksums first.
@@ -94,7 +95,7 @@ def draw_checksums(kind, t):
 
 
 def oracle_bound64(fx_out, rays, light_rays, pix, light_pixels, ppc, light, draws, cfg,
-                   ref_grads, probes):
+                   ref_grads, probes, grad_on_light):
     """Per parameter tensor: |g_ref32 - g_oracle64| / |g_ref32|, full tensor and
     on the recorded probes -- the same step (same draws) in float64."""
     wh, S, I, LI, method, sigma_bias, perturb, noise_std = cfg
@@ -105,7 +106,8 @@ def oracle_bound64(fx_out, rays, light_rays, pix, light_pixels, ppc, light, draw
     rng = O.ReplayRNG([d for _, d in draws])
     rng._queue = [q.to(dt) for q in rng._queue]
     cam = SO.render_rays(params, rays.to(dt), S, False, perturb, noise_std, I, rng=rng)
-    lres = SO.render_rays(params, light_rays.to(dt), S, False, perturb, noise_std, LI, rng=rng)
+    with torch.set_grad_enabled(grad_on_light):     # the reference's light render mode
+        lres = SO.render_rays(params, light_rays.to(dt), S, False, perturb, noise_std, LI, rng=rng)
     assert rng.exhausted()
     ppc64 = {"eye_pos": ppc["eye_pos"].to(dt), "camera": ppc["camera"].to(dt)}
     out = SO.efficient_sm(pix.to(dt), light_pixels.to(dt), cam, lres, ppc64,
@@ -244,7 +246,7 @@ def run_case(ref, name, wh, runs, N_samples, N_importance, light_importance, met
         del models, cam_res, light_res, cam_out, loss
         oracle_bound64(out, rays, light_rays, pix, pixels, ppc, light, rec.draws,
                        (wh, N_samples, N_importance, light_importance, method, sigma_bias,
-                        perturb, noise_std), ref_grads, probes)
+                        perturb, noise_std), ref_grads, probes, grad_on_light)
     os.makedirs(OUT, exist_ok=True)
     path = os.path.join(OUT, f"{name}.npz")
     np.savez_compressed(path, **out)
@@ -271,6 +273,9 @@ CASES = {
     # cfg5-shaped: 64^2 light image, 512 camera rays in three runs, 64 + 64
     "cfg5_sm2": (64, [(0, 200), (1, 180), (0, 132)], 64, 64, 64, "shadow_method_2",
                  dict(sigma_bias=0.5, noise_std=0.0, store_draws=False, seed=78)),
+    # BASELINE configs[4] exactly: the 128x128 light image (16,384 light rays)
+    "cfg5_128_sm2": (128, [(0, 300), (1, 212)], 64, 64, 64, "shadow_method_2",
+                     dict(sigma_bias=0.5, noise_std=0.0, store_draws=False, seed=80)),
     "cfg5_gol_sm2": (64, [(1, 256), (0, 256)], 64, 64, 64, "shadow_method_2",
                      dict(sigma_bias=0.5, noise_std=0.0, store_draws=False, seed=79,
                           grad_on_light=True, n_probe=2048)),
