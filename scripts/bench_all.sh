@@ -4,8 +4,10 @@
 set -u
 mkdir -p gpurun_out
 steps=${1:-20}; cpu=${2:-12}
-for c in cfg2 cfg3 cfg4 cfg5 eval; do
-    timeout -k 10 300 python bench.py --config $c --steps $steps --warmup 5 \
+for c in cfg2 cfg3 cfg4 cfg5 cfg5gol eval; do
+    args="--config $c"
+    [ $c = cfg5gol ] && args="--config cfg5 --grad-on-light"
+    timeout -k 10 300 python bench.py $args --steps $steps --warmup 5 \
         --cpu-baseline-seconds $cpu > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err
     rc=$?
     echo "$c rc=$rc"
