@@ -344,9 +344,10 @@ def cpu_eval(args, budget_s, rays_all):
 def cpu_shadow(args, budget_s, scene):
     """cfg5 on the CPU oracle, timed in two parts on bounded samples -- the
     camera part (sigma-only render of b rays + efficient_sm against a light
-    map + MSE backward + Adam) and the no_grad light render (per ray) -- then
-    combined into the step rate of the full workload (512 camera rays + the
-    whole light image per step)."""
+    map + MSE backward + Adam) and the light render (per ray: no_grad, or with
+    autograd and its backward under --grad-on-light) -- then combined into the
+    step rate of the full workload (512 camera rays + the whole light image per
+    step)."""
     from oracle import nerf_oracle as O
     from oracle import shadow_oracle as SO
     threads = _cpu_threads()
@@ -360,9 +361,15 @@ def cpu_shadow(args, budget_s, scene):
     bl = 256
     light_map = {"depth_coarse": torch.full((wh * wh,), 4.0), "depth_fine": torch.full((wh * wh,), 4.0)}
 
+    LI = max(args.light_importance, 0) if args.light_importance != -1 else 16
+
     def light_part():
-        with torch.no_grad():
-            SO.render_rays(params, lrays[:bl], S, False, 1.0, 0.0, I, 32768, False)
+        # --grad_on_light: the light render under autograd and its backward
+        with torch.set_grad_enabled(args.grad_on_light):
+            res = SO.render_rays(params, lrays[:bl], S, False, 1.0, 0.0, LI, 32768, False)
+        if args.grad_on_light:
+            opt.zero_grad()
+            sum(v.sum() for k, v in res.items() if k.startswith("depth")).backward()
     b = 64
 
     def cam_part():
@@ -372,7 +379,7 @@ def cpu_shadow(args, budget_s, scene):
                "camera": scene["mats"][0].cpu().expand(b, 3, 3)}
         res = SO.render_rays(params, rays, S, False, 1.0, 0.0, I, 32768, False)
         out = SO.efficient_sm(scene["pixels"][sel].cpu(), lpix, res, light_map, ppc, leye, lcam,
-                              (wh, wh), I > 0, I > 0, "shadow_method_2")
+                              (wh, wh), I > 0, LI > 0, "shadow_method_2")
         tgt = torch.rand(b, 3)
         loss = torch.mean((out["rgb_coarse"] - tgt) ** 2) + torch.mean((out["rgb_fine"] - tgt) ** 2)
         opt.zero_grad()
@@ -383,9 +390,11 @@ def cpu_shadow(args, budget_s, scene):
     t_cam, t_light = elc / (nc * b), ell / (nl * bl)
     t_step = args.batch * t_cam + wh * wh * t_light
     return dict(value=args.batch / t_step, unit="camera rays/s", cores=threads, kind="port",
-                sample=f"camera part {nc} x {b} rays in {elc:.1f} s, light render {nl} x {bl} rays "
-                       f"in {ell:.1f} s (oracle, torch CPU {threads} threads), combined per step "
-                       f"as {args.batch} camera rays + {wh * wh} light rays")
+                host=host_cpus(),
+                sample=f"camera part {nc} x {b} rays in {elc:.1f} s, light render "
+                       f"{'with autograd + backward ' if args.grad_on_light else ''}{nl} x {bl} "
+                       f"rays in {ell:.1f} s (oracle, torch CPU {threads} threads), combined per "
+                       f"step as {args.batch} camera rays + {wh * wh} light rays")
 
 
 # ---------------------------------------------------------------------------
