@@ -555,6 +555,8 @@ def wl_shadow(args, dev, rank):
     tgt_pool = torch.rand(total, 3, device=dev)
     light_ppc = {"eye_pos": scene["light_eye"], "camera": scene["light_cam"]}
     loss_fn = MSELoss()                       # train_efficient_sm.py's loss_dict['mse']
+    from nerf_pl_amd.losses import OpactiyLoss
+    opacity_fn = OpactiyLoss()                # :43, evaluated (logged, not trained) at :191
     # Light_N_importance == -1: np.random.choice([0, 8, 16, 32]) per light render
     # (:153-154); one generator seeded alike on every rank keeps the ranks'
     # light renders the same shape (the sharded render gathers them)
@@ -580,7 +582,10 @@ def wl_shadow(args, dev, rank):
                                        32768, False, were_gradients_computed=False)
         out = RS.efficient_sm(scene["pixels"][sel % hw], scene["light_pixels"], cam, light, ppc,
                               light_ppc, (wh, wh), I > 0, li > 0, "shadow_method_2")
-        return loss_fn(out, tgt_pool[sel])
+        tgt = tgt_pool[sel]
+        with torch.no_grad():                 # log['train/train_opactiy'] (:191-195)
+            opacity_fn(light, tgt)
+        return loss_fn(out, tgt)
 
     lname = "random {0,8,16,32}" if LI == -1 else str(LI)
     # light samples per light ray: coarse S, plus S + li fine when li > 0
@@ -596,6 +601,7 @@ def wl_shadow(args, dev, rank):
                          f"({S}+{lname}"
                          f"{', sharded over the ranks + all-gather' if args.light_shard else ''}) + efficient_sm "
                          "(shadow_method_2, per-pose runs) + MSE + backward"
+                         " + the logged OpactiyLoss"
                          f"{' (through the light render too)' if gol else ''} + Adam lr 5e-4",
                 data=f"synthetic ({args.poses}-pose camera orbit + one light camera, rays "
                      "generated on device, random targets, seeded default-init NeRF pair)",
