@@ -5,6 +5,7 @@ Groups of scripts/psnr_compare.py runs (2000 steps, PSNR at 500/1000/1500/2000,
 fine rgb on 2 held-out views; unperturbed runs only):
   f16x3      this package, default arithmetic   profiles/r03/psnr/f16x3_s*.json
   fp32       this package, exact fp32 MFMA      profiles/r03/psnr/fp32_s*.json
+  bf16       this package, the reduced-precision bf16 variant   profiles/r03/psnr/bf16_s*.json
   ref_gpu    the reference's algorithm in PyTorch fp32 on the MI355X (the oracle,
              pinned bit-exact to the reference; hipBLAS GEMMs)   profiles/r03/psnr/oracle_s*.json
   ref_cpu    the reference itself, CPU, here    profiles/r01/psnr_reference_s*.json,
@@ -59,6 +60,7 @@ def main():
     groups = {
         "f16x3": load("profiles/r03/psnr/f16x3_s*.json"),
         "fp32": load("profiles/r03/psnr/fp32_s*.json"),
+        "bf16": load("profiles/r03/psnr/bf16_s*.json"),
         "ref_gpu": load("profiles/r03/psnr/oracle_s*.json"),
         "ref_cpu": load("profiles/r01/psnr_reference_s*.json", "profiles/r02/psnr/reference_s*.json",
                         "profiles/r03/psnr/reference_s*.json"),
@@ -66,7 +68,8 @@ def main():
     groups["ref_all"] = {("g", s): v for s, v in groups["ref_gpu"].items()}
     groups["ref_all"].update({("c", s): v for s, v in groups["ref_cpu"].items()})
     pairs = [("f16x3", "ref_all"), ("fp32", "ref_all"), ("f16x3", "ref_gpu"), ("f16x3", "ref_cpu"),
-             ("fp32", "ref_gpu"), ("f16x3", "fp32"), ("ref_gpu", "ref_cpu")]
+             ("fp32", "ref_gpu"), ("f16x3", "fp32"), ("ref_gpu", "ref_cpu"), ("bf16", "ref_all"),
+             ("bf16", "f16x3")]
     out = {"groups": {k: sorted(map(str, v)) for k, v in groups.items()}, "checkpoints": []}
     for step in STEPS:
         row = {"step": step, "groups": {}, "diffs": {}}
