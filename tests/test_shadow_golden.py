@@ -58,24 +58,41 @@ def n_models(cfg):
     return 2 if cfg["N_importance"] > 0 or cfg["light_importance"] > 0 else 1
 
 
-def run_oracle(fx, requires_grad=False, dtype=torch.float32):
+def n_camera_draws(cfg):
+    """draws of the camera render (rendering.py order): rand(B,S) if perturb,
+    randn(B,S), and rand(B,I), rand_like(B,I), randn(B,S+I) if I > 0"""
+    return (1 if cfg["perturb"] > 0 else 0) + 1 + (3 if cfg["N_importance"] > 0 else 0)
+
+
+def run_oracle(fx, requires_grad=False, dtype=torch.float32, light_rows=None):
+    """The oracle's training step on a fixture.  ``light_rows=k``: the light
+    render is checked on its first k rows only (rendered with those rows of
+    the draws -- rays are independent) and efficient_sm reads the fixture's
+    (the reference's) light maps; the light outputs returned are the k rows."""
     cfg = shadow_cfg(fx)
     params = [{k: v.to(dtype) for k, v in O.make_params(s, sigma_bias=cfg["sigma_bias"]).items()}
               for s in cfg["seeds"][:n_models(cfg)]]
     if requires_grad:
         params = [{k: v.requires_grad_(True) for k, v in p.items()} for p in params]
-    rng = O.ReplayRNG(fixture_draws(fx))
+    draws = fixture_draws(fx)
+    nc = n_camera_draws(cfg)
+    if light_rows is not None:
+        draws = draws[:nc] + [d[:light_rows] for d in draws[nc:]]
+    rng = O.ReplayRNG(draws)
     rng._queue = [q.to(dtype) for q in rng._queue]
 
     def t(k):
         return torch.from_numpy(fx[k]).to(dtype)
     cam = SO.render_rays(params, t("rays"), cfg["N_samples"], False, cfg["perturb"],
                          cfg["noise_std"], cfg["N_importance"], rng=rng)
+    lrays = t("light_rays") if light_rows is None else t("light_rays")[:light_rows]
     with torch.set_grad_enabled(requires_grad and cfg["grad_on_light"]):
-        light = SO.render_rays(params, t("light_rays"), cfg["N_samples"], False,
+        light = SO.render_rays(params, lrays, cfg["N_samples"], False,
                                cfg["perturb"], cfg["noise_std"], cfg["light_importance"],
                                rng=rng)
     assert rng.exhausted()
+    light_in = light if light_rows is None else \
+        {k[6:]: t(k) for k in fx if k.startswith("light_depth")}
     depths, light_depths = {}, {}
     for k in ("depth_coarse", "depth_fine"):
         if k in cam and requires_grad:
@@ -85,7 +102,7 @@ def run_oracle(fx, requires_grad=False, dtype=torch.float32):
             light[k].retain_grad()
             light_depths[k] = light[k]
     ppc = {"eye_pos": t("eye_pos"), "camera": t("camera")}
-    out = SO.efficient_sm(t("pixels"), t("light_pixels"), cam, light, ppc,
+    out = SO.efficient_sm(t("pixels"), t("light_pixels"), cam, light_in, ppc,
                           t("light_eye"), t("light_camera"), (cfg["wh"], cfg["wh"]),
                           cfg["N_importance"] > 0, cfg["light_importance"] > 0, cfg["method"])
     return cfg, params, cam, light, out, depths, light_depths
@@ -94,10 +111,16 @@ def run_oracle(fx, requires_grad=False, dtype=torch.float32):
 @pytest.mark.parametrize("case", CASES)
 def test_shadow_oracle_forward_matches(case):
     fx = load_shadow(case)
+    # cfg5-shaped fixtures: the light image (4,096 / 16,384 rays) checked on its
+    # first 1,024 rows, the shadow stage on the reference's whole light maps --
+    # the full light render would take minutes of CPU in this suite
+    rows = 1024 if case.startswith("cfg5") else None
     with torch.no_grad():
-        _, _, _, light, out, _, _ = run_oracle(fx)
+        _, _, _, light, out, _, _ = run_oracle(fx, light_rows=rows)
     for k, v in list(out.items()) + [("light_" + k, v) for k, v in light.items()]:
         ref = fx[k if k.startswith("light_") else f"out_{k}"]
+        if k.startswith("light_") and rows is not None:
+            ref = ref[:rows]
         np.testing.assert_allclose(v.detach().numpy(), ref, rtol=1e-5,
                                    atol=1e-6 * max(1.0, float(np.abs(ref).max())), err_msg=k)
 
