@@ -330,9 +330,14 @@ def test_efficient_sm_training_step_matches_reference(case):
     """train_efficient_sm.py:139-202 end to end through the drop-in API,
     replaying the reference's draws: sigma-only camera render + light render
     (under autograd for --grad_on_light) + efficient_sm + MSE + backward."""
+    check_training_step(case, load_shadow(case))
+
+
+def check_training_step(case, fx):
+    """The step against a reference record ``fx`` (a golden fixture, or the
+    oracle's record of a random configuration: tests/test_gpu_shadow_random.py)."""
     from nerf_pl_amd import ReplayRNG
     from nerf_pl_amd import rendering_shadows as RS
-    fx = load_shadow(case)
     cfg = shadow_cfg(fx)
     wh, method = cfg["wh"], cfg["method"]
     draws = fixture_draws(fx)

@@ -1,0 +1,148 @@
+"""Randomised configurations of the shadow-mapping training step (config 5),
+with and without --grad_on_light, against the oracle (oracle/shadow_oracle.py,
+pinned to the reference by tests/test_shadow_golden.py) -- the less travelled
+combinations of light-map size, sample counts, light importance, shadow
+method, noise, perturbation and per-pose runs that the golden fixtures do not
+hold.  Each configuration becomes a reference record of the same form as a
+golden fixture (the oracle's fp32 outputs and gradients, and the float64
+oracle's distance from them as the noise floor) and goes through the same
+check as the fixtures (tests/test_gpu_shadow.py::check_training_step): 1e-4 on
+every output, every screened ray explained, gradients within the noise-floor
+bound."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+from oracle import rays_oracle as RO
+from oracle import shadow_oracle as SO
+from test_gpu_shadow import check_training_step
+
+pytestmark = pytest.mark.gpu
+
+
+def _config(seed):
+    r = np.random.default_rng(seed)
+    return dict(wh=int(r.choice([8, 12, 16, 24])), S=int(r.integers(6, 33)),
+                I=int(r.choice([0, int(r.integers(4, 33))])),
+                LI=int(r.choice([0, int(r.integers(4, 25))])),
+                method=int(r.integers(1, 3)), sigma_bias=float(r.uniform(0.3, 1.2)),
+                perturb=float(r.choice([0.0, 1.0])), noise=float(r.choice([0.0, 1.0])),
+                gol=bool(seed % 2 == 0),
+                runs=[(int(r.integers(0, 2)), int(r.integers(3, 60))) for _ in range(int(r.integers(1, 4)))],
+                seed=seed)
+
+
+def _scene(c):
+    from nerf_pl_amd.camera import Camera
+    from nerf_pl_amd.rays import LEGO_CAMERA_ANGLE_X, blender_focal, pose_spherical
+    wh = c["wh"]
+    focal = blender_focal(wh)
+    hfov = LEGO_CAMERA_ANGLE_X * 180. / np.pi
+    dirs = RO.get_ray_directions(wh, wh, focal)
+
+    def rays_of(c2w):
+        o, d = RO.get_rays(dirs, c2w)
+        return torch.cat([o, d, torch.ones_like(o[:, :1]), 200. * torch.ones_like(o[:, :1])], 1)
+    l2w = pose_spherical(35.0 + c["seed"], -55.0, 4.0)
+    light = Camera(hfov, (wh, wh))
+    light.set_pose_using_blender_matrix(l2w, False)
+    i, j = np.meshgrid(np.arange(wh), np.arange(wh), indexing="xy")
+    pixels = torch.stack([torch.tensor(i) + 0.5, torch.tensor(j) + 0.5,
+                          torch.ones(wh, wh, dtype=torch.float64)], -1).view(-1, 3).float()
+    cams = []
+    for theta in (-20.0 + 3 * c["seed"], 60.0):
+        c2w = pose_spherical(theta, -30.0, 4.0)
+        cam = Camera(hfov, (wh, wh))
+        cam.set_pose_using_blender_matrix(c2w, False)
+        cams.append((cam, rays_of(c2w)))
+    return light, rays_of(l2w), pixels, cams
+
+
+def _record(c):
+    """a golden-fixture-shaped record of the oracle's step"""
+    g = torch.Generator().manual_seed(1000 + c["seed"])
+    light, lrays, pixels, cams = _scene(c)
+    rays, pix, eyes, mats = [], [], [], []
+    for pose, count in c["runs"]:
+        cam, crays = cams[pose]
+        idx = torch.randperm(crays.shape[0], generator=g)[:count]
+        rays.append(crays[idx]); pix.append(pixels[idx])
+        eyes.append(cam.eye_pos.float().expand(count, 3))
+        mats.append(cam.camera.float().expand(count, 3, 3))
+    rays, pix = torch.cat(rays).contiguous(), torch.cat(pix).contiguous()
+    n, nl, S, I, LI = rays.shape[0], lrays.shape[0], c["S"], c["I"], c["LI"]
+
+    def draws_for(m, I_):
+        d = [torch.rand(m, S, generator=g)] if c["perturb"] > 0 else []
+        d.append(torch.randn(m, S, generator=g))
+        if I_ > 0:
+            d += [torch.rand(m, I_, generator=g), torch.rand(m, I_, generator=g),
+                  torch.randn(m, S + I_, generator=g)]
+        return d
+    draws = draws_for(n, I) + draws_for(nl, LI)
+    target = torch.rand(n, 3, generator=g)
+    method = "shadow_method_1" if c["method"] == 1 else "shadow_method_2"
+    fx = {"cfg": np.array([c["wh"], S, I, LI, c["method"], c["sigma_bias"], c["perturb"],
+                           c["noise"], 51, 52, 1 if c["gol"] else 0], dtype=np.float64),
+          "rays": rays.numpy(), "pixels": pix.numpy(), "light_rays": lrays.float().numpy(),
+          "light_pixels": pixels.numpy(), "eye_pos": torch.cat(eyes).numpy(),
+          "camera": torch.cat(mats).numpy(), "light_eye": light.eye_pos.float().numpy(),
+          "light_camera": light.camera.float().numpy(), "target": target.numpy(),
+          "n_draws": np.array(len(draws))}
+    for k, d in enumerate(draws):
+        fx[f"draw{k}"] = d.numpy()
+
+    def step(dt):
+        n_models = 2 if I > 0 or LI > 0 else 1
+        params = [{k: v.to(dt).requires_grad_(True)
+                   for k, v in O.make_params(s, sigma_bias=c["sigma_bias"]).items()}
+                  for s in (51, 52)[:n_models]]
+        rng = O.ReplayRNG(draws)
+        rng._queue = [q.to(dt) for q in rng._queue]
+        cam = SO.render_rays(params, rays.to(dt), S, False, c["perturb"], c["noise"], I, rng=rng)
+        with torch.set_grad_enabled(c["gol"]):
+            lres = SO.render_rays(params, lrays.to(dt), S, False, c["perturb"], c["noise"], LI,
+                                  rng=rng)
+        for k in ("depth_coarse", "depth_fine"):
+            if c["gol"] and k in lres:
+                lres[k].retain_grad()
+        ppc = {"eye_pos": torch.cat(eyes).to(dt), "camera": torch.cat(mats).to(dt)}
+        out = SO.efficient_sm(pix.to(dt), pixels.to(dt), cam, lres, ppc,
+                              light.eye_pos.to(dt), light.camera.to(dt), (c["wh"], c["wh"]),
+                              I > 0, LI > 0, method)
+        t = target.to(dt)
+        loss = torch.mean((out["rgb_coarse"] - t) ** 2)
+        if "rgb_fine" in out:
+            loss = loss + torch.mean((out["rgb_fine"] - t) ** 2)
+        loss.backward()
+        return params, out, lres, loss
+    p32, out32, l32, loss32 = step(torch.float32)
+    p64, _, _, _ = step(torch.float64)
+    fx["loss"] = np.array(loss32.item())
+    for k, v in out32.items():
+        fx[f"out_{k}"] = v.detach().numpy()
+    for k, v in l32.items():
+        fx[f"light_{k}"] = v.detach().numpy()
+        if c["gol"] and k.startswith("depth") and v.grad is not None:
+            fx[f"grad_light_{k}"] = v.grad.numpy()
+    for m, (a, b) in enumerate(zip(p32, p64)):
+        for name in a:
+            if a[name].grad is None:
+                continue
+            g32 = a[name].grad.numpy()
+            g64 = b[name].grad.numpy() if b[name].grad is not None else np.zeros(g32.shape)
+            d32 = g32.astype(np.float64)
+            key = f"grad{m}_{name}"
+            fx[key + "_sum"] = np.array(g32.astype(np.float64).sum())
+            fx[key + "_l2"] = np.array(np.linalg.norm(g32.astype(np.float64)))
+            fx[key + "_full"] = g32
+            fx[key + "_bound64"] = np.array(np.linalg.norm(d32 - g64) / (np.linalg.norm(d32) + 1e-300))
+    return fx
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_shadow_step_matches_oracle(seed):
+    c = _config(seed)
+    print(c)
+    check_training_step(f"random{seed}", _record(c))
