@@ -435,7 +435,11 @@ def check_training_step(case, fx):
                 continue
             ref = fx["grad_light_" + k]
             got = light[k].grad.cpu().numpy()
-            np.testing.assert_allclose(got, ref, rtol=1e-3, atol=1e-5 * np.abs(ref).max(),
+            # records that carry it: twice the reference's own fp32 noise (exact
+            # cancellations at a run's extremes leave rounding residues)
+            noise = 2.0 * float(fx.get("grad_light_" + k + "_noise64", 0.0))
+            np.testing.assert_allclose(got, ref, rtol=1e-3,
+                                       atol=max(1e-5 * np.abs(ref).max(), noise),
                                        err_msg=f"{case}: d loss / d light {k}")
     for m, net in enumerate(models):
         for name, p in net.named_parameters():

@@ -118,7 +118,7 @@ def _record(c):
         loss.backward()
         return params, out, lres, loss
     p32, out32, l32, loss32 = step(torch.float32)
-    p64, _, _, _ = step(torch.float64)
+    p64, _, l64, _ = step(torch.float64)
     fx["loss"] = np.array(loss32.item())
     for k, v in out32.items():
         fx[f"out_{k}"] = v.detach().numpy()
@@ -126,6 +126,10 @@ def _record(c):
         fx[f"light_{k}"] = v.detach().numpy()
         if c["gol"] and k.startswith("depth") and v.grad is not None:
             fx[f"grad_light_{k}"] = v.grad.numpy()
+            # the fp32 reference's absolute noise: a texel read only by its run's
+            # min ray gets gc/b - S_a/cnt = 0 exactly, in fp32 a rounding residue
+            fx[f"grad_light_{k}_noise64"] = np.array(
+                np.abs(v.grad.numpy().astype(np.float64) - l64[k].grad.numpy()).max())
     for m, (a, b) in enumerate(zip(p32, p64)):
         for name in a:
             if a[name].grad is None:
