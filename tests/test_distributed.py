@@ -64,8 +64,13 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_grad_allreduce_matches_single_process():
-    world = 2
+import pytest
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_grad_allreduce_matches_single_process(world):
+    """world 8: the rank count of the driver's 8-GPU run (cfg4), one sample per
+    rank, over gloo on the CPU"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -240,12 +245,13 @@ def _run(world, target, *args):
     return res
 
 
-def test_sharded_map_backward_reduce_scatters():
+@pytest.mark.parametrize("world,n", [(2, 7), (8, 7), (8, 29)])
+def test_sharded_map_backward_reduce_scatters(world, n):
     """--grad_on_light with the light image sharded: the gathered rows stay
     differentiable, and each rank's parameter gradient is what it gets from the
     rows it rendered under every rank's loss -- so the all-reduced average
-    equals the reference's (every rank renders every row, DDP averages)."""
-    world, n = 2, 7
+    equals the reference's (every rank renders every row, DDP averages).
+    (8, 7): a rank with no rows of its own."""
     res = _run(world, _shard_grad_worker, n, False)
     x = torch.arange(n * 3, dtype=torch.float32).view(n, 3)
     per = (n + world - 1) // world
@@ -253,7 +259,7 @@ def test_sharded_map_backward_reduce_scatters():
     total = torch.zeros(3)
     for rank, status, g in res:
         assert status == "ok"
-        lo, hi = rank * per, min(n, (rank + 1) * per)
+        lo, hi = min(n, rank * per), min(n, (rank + 1) * per)
         exp = (coef_sum[lo:hi, None] * x[lo:hi]).sum(0)
         torch.testing.assert_close(g, exp, rtol=1e-6, atol=1e-6)
         total += g
@@ -308,3 +314,20 @@ def test_ray_sampler_partitions_epochs_like_distributed_sampler():
         torch.testing.assert_close(e, perm[rank::world], rtol=0, atol=0)
     # the second epoch is a different permutation
     assert not torch.equal(res[0][1][steps], res[0][1][0])
+
+
+def test_ray_sampler_matches_distributed_sampler_at_eight_ranks():
+    """the 8-rank partition of an epoch whose size the world does not divide
+    (padded with the permutation's head, DistributedSampler(drop_last=False)),
+    over two epochs, against torch.utils.data.DistributedSampler itself"""
+    from torch.utils.data import DistributedSampler
+    world, total, batch = 8, 100, 13            # 100 % 8 = 4 -> 4 padded indices
+    steps = 1                                   # ceil(100 / 8) = 13 per rank per epoch
+    res = _run(world, _sampler_worker, total, batch, 2 * steps)
+    for rank, batches, epoch in res:
+        assert epoch == 1
+        for e in range(2):
+            ds = DistributedSampler(range(total), num_replicas=world, rank=rank, shuffle=True,
+                                    seed=7, drop_last=False)
+            ds.set_epoch(e)
+            assert batches[e].tolist() == list(ds), (rank, e)
