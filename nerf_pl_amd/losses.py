@@ -164,8 +164,13 @@ loss_dict = {"mse": MSELoss, "sm": SMMSELoss, "opacity": OpactiyLoss}
 
 
 def mse(image_pred, image_gt, valid_mask=None, reduction="mean"):
-    """metrics.py:4-10."""
-    if valid_mask is not None or reduction != "mean":
+    """metrics.py:4-10.  float32 device tensors go through the HIP kernel; any
+    other operands -- eval.py:143 passes a CPU tensor and a numpy image -- take
+    the reference's own expression (evaluation glue, not the training path)."""
+    dev = (isinstance(image_pred, torch.Tensor) and isinstance(image_gt, torch.Tensor)
+           and image_pred.is_cuda and image_gt.is_cuda
+           and image_pred.dtype == torch.float32 and image_gt.dtype == torch.float32)
+    if valid_mask is not None or reduction != "mean" or not dev:
         value = (image_pred - image_gt) ** 2
         if valid_mask is not None:
             value = value[valid_mask]

@@ -139,12 +139,37 @@ def main():
     ap.add_argument("--eval-weights", default=None,
                     help="no training: render the held-out views with these trained "
                          "parameters and report the PSNR (same-weights renderer parity)")
+    ap.add_argument("--draw-seeds", default=None,
+                    help="a range lo-hi of draw seeds run one after another in this process "
+                         "(with --out-dir)")
+    ap.add_argument("--out-dir", default="gpurun_out/psnr")
     ap.add_argument("--out", default=None, help="JSON path (default profiles/r01/psnr_<impl>.json)")
     args = ap.parse_args()
     torch.set_num_threads(args.threads or min(16, os.cpu_count() or 1))
     S, I = 64, 64
     train, train_rgb, test, test_rgb = scene()
+    if args.draw_seeds:
+        # several runs in one process (the scene's ground truth is built once);
+        # one JSON per seed under --out-dir, named like scripts/psnr_r03.sh's
+        lo, _, hi = args.draw_seeds.partition("-")
+        seeds = range(int(lo), int(hi or lo) + 1)
+        if args.impl == "ours":
+            from nerf_pl_amd import ops
+            tag = ops.MATH
+        else:
+            tag = args.impl
+        os.makedirs(args.out_dir, exist_ok=True)
+        for sd in seeds:
+            args.draw_seed = sd
+            args.out = os.path.join(args.out_dir, f"{tag}_s{sd}.json")
+            run_one(args, S, I, train, train_rgb, test, test_rgb)
+        return
+    run_one(args, S, I, train, train_rgb, test, test_rgb)
 
+
+
+def run_one(args, S, I, train, train_rgb, test, test_rgb):
+    """one training run (models, optimiser and draws from args.draw_seed)"""
     if args.impl == "ours":
         from nerf_pl_amd import Embedding, NeRF, render_rays
         dev = torch.device("cuda", 0)

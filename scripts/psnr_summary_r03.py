@@ -12,7 +12,12 @@ fine rgb on 2 held-out views; unperturbed runs only):
              profiles/r02/psnr/reference_s*.json, profiles/r03/psnr/reference_s*.json
 Per checkpoint: each group's n / mean / std, and for every pair the difference
 of the means, its standard error (Welch), the 95% interval and whether that
-interval lies inside +-0.1 dB.  Writes profiles/r03/psnr/summary.json.
+interval lies inside +-0.1 dB.  Paired too ("paired"): runs of the same draw
+seed start from the same parameters and see the same ray batches and the same
+render draws, so their PSNRs are correlated (r ~ 0.5-0.7) and the per-seed
+difference has a smaller spread than two independent samples; mean and
+Student-t interval of the per-seed differences over the seeds both groups ran.
+Writes profiles/r03/psnr/summary.json.
 
     python scripts/psnr_summary_r03.py
 """
@@ -70,6 +75,8 @@ def main():
     pairs = [("f16x3", "ref_all"), ("fp32", "ref_all"), ("f16x3", "ref_gpu"), ("f16x3", "ref_cpu"),
              ("fp32", "ref_gpu"), ("f16x3", "fp32"), ("ref_gpu", "ref_cpu"), ("bf16", "ref_all"),
              ("bf16", "f16x3")]
+    paired = [("f16x3", "ref_gpu"), ("fp32", "ref_gpu"), ("bf16", "ref_gpu"), ("f16x3", "fp32"),
+              ("f16x3", "ref_cpu"), ("ref_gpu", "ref_cpu")]
     out = {"groups": {k: sorted(map(str, v)) for k, v in groups.items()}, "checkpoints": []}
     for step in STEPS:
         row = {"step": step, "groups": {}, "diffs": {}}
@@ -92,6 +99,24 @@ def main():
             row["diffs"][f"{a}-{b}"] = {
                 "diff": round(d, 3), "se": round(se, 3), "ci95": [round(d - half, 3), round(d + half, 3)],
                 "ci95_within_0.1dB": bool(abs(d) + half <= 0.1), "n": [na, nb]}
+        row["paired"] = {}
+        for a, b in paired:
+            common = sorted(s for s in set(groups[a]) & set(groups[b])
+                            if step in groups[a][s] and step in groups[b][s])
+            if len(common) < 3:
+                continue
+            ds = [groups[a][s][step] - groups[b][s][step] for s in common]
+            n, m, sd = stats(ds)
+            se = sd / math.sqrt(n)
+            half = t975(n - 1) * se
+            xa = [groups[a][s][step] for s in common]
+            xb = [groups[b][s][step] for s in common]
+            _, ma, sa = stats(xa)
+            _, mb, sb = stats(xb)
+            r = sum((x - ma) * (y - mb) for x, y in zip(xa, xb)) / ((n - 1) * sa * sb)
+            row["paired"][f"{a}-{b}"] = {
+                "diff": round(m, 3), "se": round(se, 3), "ci95": [round(m - half, 3), round(m + half, 3)],
+                "ci95_within_0.1dB": bool(abs(m) + half <= 0.1), "n": n, "corr": round(r, 2)}
         out["checkpoints"].append(row)
         print(json.dumps(row))
     path = os.path.join(REPO, "profiles", "r03", "psnr", "summary.json")
