@@ -1,0 +1,89 @@
+"""Zero fraction of the saved activations and gradient segments that the f16x3
+weight gradient streams ("levers"): how many of the bytes it
+reads are ReLU zeros, at the bench's default init and with trained weights.
+
+    NERF_PL_AMD_DEBUG=1 python dev/sparsity.py [--weights trained.safetensors] [--out f.json]
+
+One training render per model (128 stratified samples per ray, 4,096 rays of
+the PSNR scene's training views, targets = the scene), backward, then the
+buffers `functions._DEBUG` keeps: per segment, the fraction of exact zeros.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "scripts"))
+
+W32 = 32  # samples per block
+
+
+def seg_zero(buf, off, width, nb):
+    x = buf[off:off + width * W32 * nb]
+    return float((x == 0).float().mean())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--weights", default=None)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    assert os.environ.get("NERF_PL_AMD_DEBUG") == "1", "run with NERF_PL_AMD_DEBUG=1"
+    import psnr_compare as pc
+    from nerf_pl_amd import Embedding, NeRF, functions, ops, render_rays
+    dev = torch.device("cuda", 0)
+    train, train_rgb, _, _ = pc.scene()
+    g = torch.Generator().manual_seed(0)
+    idx = torch.randint(0, train.shape[0], (4096,), generator=g)
+    rays, tgt = train[idx].to(dev), train_rgb[idx].to(dev)
+    emb = [Embedding(3, 10), Embedding(3, 4)]
+    res = {"weights": os.path.basename(args.weights) if args.weights else "default init"}
+    sd = None
+    if args.weights:
+        from safetensors.torch import load_file
+        sd = load_file(args.weights)
+    for tag, seed in (("coarse", 101), ("fine", 102)):
+        m = NeRF()
+        m.load_state_dict(pc.initial_params(seed, False))
+        if sd is not None:
+            m.load_state_dict({k[len(tag) + 1:]: v for k, v in sd.items() if k.startswith(tag + ".")})
+        m = m.to(dev)
+        out = render_rays([m], emb, rays, 128, False, 1, 0, 0, 32768, False, False)
+        loss = torch.mean((out["rgb_coarse"] - tgt) ** 2)
+        loss.backward()
+        d = functions._DEBUG
+        n = d["n"]
+        nb = ops.n_blocks(n)
+        save, gws = d["save"], d["grad_ws"]
+        r = {"samples": n}
+        r["pe"] = seg_zero(save, 0, 64, nb)
+        for l in range(8):
+            r[f"h{l + 1}"] = seg_zero(save, (64 + l * 256) * W32 * nb, 256, nb)
+        r["feat"] = seg_zero(save, (64 + 8 * 256) * W32 * nb, 256, nb)
+        r["hdir"] = seg_zero(save, (64 + 9 * 256) * W32 * nb, 128, nb)
+        for l in range(8):
+            r[f"dz{l + 1}"] = seg_zero(gws, l * 256 * W32 * nb, 256, nb)
+        r["dfeat"] = seg_zero(gws, 8 * 256 * W32 * nb, 256, nb)
+        r["dzdir"] = seg_zero(gws, 9 * 256 * W32 * nb, 128, nb)
+        # the wgrad operand bytes (19,856 B/sample): values that are zero
+        widths = {"pe": 64, "feat": 256, "hdir": 128, "dfeat": 256, "dzdir": 128}
+        widths.update({f"h{l + 1}": 256 for l in range(8)})
+        widths.update({f"dz{l + 1}": 256 for l in range(8)})
+        tot = sum(widths.values()) + 32 + 4 + 0   # + dir PE (32) + head (4): never zero
+        r["zero_fraction_of_wgrad_values"] = round(
+            sum(r[k] * w for k, w in widths.items()) / tot, 4)
+        res[tag] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
+        print(tag, json.dumps(res[tag]), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -140,9 +140,12 @@ def main():
                     help="no training: render the held-out views with these trained "
                          "parameters and report the PSNR (same-weights renderer parity)")
     ap.add_argument("--draw-seeds", default=None,
-                    help="a range lo-hi of draw seeds run one after another in this process "
+                    help="draw seeds (comma-separated lo-hi ranges) run one after another in this process "
                          "(with --out-dir)")
     ap.add_argument("--out-dir", default="gpurun_out/psnr")
+    ap.add_argument("--deadline-s", type=float, default=0,
+                    help="with --draw-seeds: start no further seed once this many seconds "
+                         "have passed since the first one started (the time-boxed GPU calls)")
     ap.add_argument("--out", default=None, help="JSON path (default profiles/r01/psnr_<impl>.json)")
     args = ap.parse_args()
     torch.set_num_threads(args.threads or min(16, os.cpu_count() or 1))
@@ -151,15 +154,21 @@ def main():
     if args.draw_seeds:
         # several runs in one process (the scene's ground truth is built once);
         # one JSON per seed under --out-dir, named like scripts/psnr_r03.sh's
-        lo, _, hi = args.draw_seeds.partition("-")
-        seeds = range(int(lo), int(hi or lo) + 1)
+        seeds = []
+        for part in args.draw_seeds.split(","):     # "lo-hi" ranges, comma-separated
+            lo, _, hi = part.partition("-")
+            seeds += range(int(lo), int(hi or lo) + 1)
         if args.impl == "ours":
             from nerf_pl_amd import ops
             tag = ops.MATH
         else:
             tag = args.impl
         os.makedirs(args.out_dir, exist_ok=True)
+        t0 = time.time()
         for sd in seeds:
+            if args.deadline_s and time.time() - t0 > args.deadline_s:
+                print(json.dumps({"deadline": args.deadline_s, "next_seed": sd}), flush=True)
+                break
             args.draw_seed = sd
             args.out = os.path.join(args.out_dir, f"{tag}_s{sd}.json")
             run_one(args, S, I, train, train_rgb, test, test_rgb)
