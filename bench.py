@@ -89,12 +89,15 @@ def kernel_roofline(k, events, math_, traffic_json):
     saved segment once at 60 FLOP/B: HBM-bound (algorithmic bytes); the fused
     forward and data-gradient chains are MFMA-bound (algorithmic FLOPs of the
     fp32 products)."""
-    big = [(s.elapsed_time(e), n) for s, e, n in events]
-    nmax = max(n for _, n in big)
-    durs = [t for t, n in big if n == nmax]
+    big = [(ev[0].elapsed_time(ev[1]), ev[2], active_samples(ev)) for ev in events]
+    nmax = max(n for _, n, _ in big)
+    durs = [t for t, n, _ in big if n == nmax]
     avg = sum(durs) / len(durs)
+    # samples the fine-pass launches actually worked on (the backward skips
+    # the blocks whose output gradient is exactly zero)
+    nwork = sum(w for _, n, w in big if n == nmax) / len(durs)
     flops = KERNEL_FLOP[k]
-    tflops = flops * nmax / (avg * 1e-3) / 1e12
+    tflops = flops * nwork / (avg * 1e-3) / 1e12
     traffic, tsrc = None, None
     t = traffic_json.get(f"{math_}/{k}") or traffic_json.get(k)
     if t and int(t["samples"]) == nmax and t.get("arithmetic", math_) == math_:
@@ -102,6 +105,10 @@ def kernel_roofline(k, events, math_, traffic_json):
         tsrc = f"{t.get('file', 'profiles/r01/traffic.json')} ({t['method']})"
     common = dict(kernel=k, traffic=traffic, traffic_unit="GB per launch", traffic_source=tsrc,
                   samples_per_launch=nmax, avg_launch_ms=round(avg, 4))
+    if nwork != nmax:
+        common["active_samples_per_launch"] = round(nwork, 1)
+        common["active_basis"] = ("achieved counts the samples the backward worked on "
+                                  "(nr_active_samples: those with a nonzero output gradient)")
     np_ = SPLIT_PRODUCTS.get(math_)
     peak = BF16_MFMA_PEAK_TF / np_ if np_ else FP32_MFMA_PEAK_TF
     # the weight gradient streams every saved segment once at 60 FLOP/B: below
@@ -111,7 +118,7 @@ def kernel_roofline(k, events, math_, traffic_json):
     if math_ == "bf16":
         bps //= 2
     if k.startswith("mlp_wgrad") and flops / bps < peak * 1e12 / (HBM_PEAK_GBS * 1e9):
-        ach = bps * nmax / (avg * 1e-3) / 1e9
+        ach = bps * nwork / (avg * 1e-3) / 1e9
         return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 4), bytes_per_sample=bps,
                     bytes_basis=("every saved activation (2528 values/sample) and gradient "
@@ -200,10 +207,23 @@ class KernelTimer:
     def summary(self):
         out = {}
         for tag, lst in self.events.items():
-            ms = [s.elapsed_time(e) for s, e, _ in lst]
+            ms = [s.elapsed_time(e) for s, e, *_ in lst]
             out[tag] = dict(launches=len(lst), total_ms=sum(ms), avg_ms=sum(ms) / len(ms),
-                            samples=sum(n for *_, n in lst) / len(lst))
+                            samples=sum(ev[2] for ev in lst) / len(lst))
+            if any(ev[3] is not None for ev in lst):
+                # the zero-gradient-block backward: samples of the listed blocks
+                out[tag]["active_samples"] = sum(active_samples(ev) for ev in lst) / len(lst)
         return out
+
+
+def active_samples(ev):
+    """samples a launch worked on: all n, or for a *_active backward entry the
+    samples nr_active_samples listed (read after the timed region)"""
+    n, act = ev[2], ev[3]
+    if act is None:
+        return n
+    sl, i = act
+    return min(n, int(sl[i].item()))
 
 
 def install_timers(timer):
@@ -211,6 +231,7 @@ def install_timers(timer):
 
     def call_tag(name, *a):
         base = name[:-3] if name[-3:] in ("_x3", "_h3", "_b1") else name
+        base = base[:-7] if base.endswith("_active") else base
         if base == "nr_mlp_fwd":
             if a[7]:     # sigma_only: inference, or the sigma-only training forward (save)
                 return ("mlp_fwd_sigma_train" if a[9] else "mlp_fwd_sigma"), int(a[3])
@@ -228,17 +249,21 @@ def install_timers(timer):
         return name[3:], 0
 
     orig_call = _lib.call
+    import nerf_pl_amd.functions as F
+    F.ACTIVE_LOG = []
 
     def timed_call(name, *a):
         if not timer.enabled:
             return orig_call(name, *a)
         tag, n = call_tag(name, *a)
+        # a *_active backward entry: the block list functions.py just built
+        act = F.ACTIVE_LOG[-1] if "_active" in name and F.ACTIVE_LOG else None
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         orig_call(name, *a)
         e.record()
-        timer.events.setdefault(tag, []).append((s, e, n))
+        timer.events.setdefault(tag, []).append((s, e, n, act))
 
     _lib.call = timed_call
     ops.call = timed_call
@@ -641,8 +666,10 @@ def main():
     from nerf_pl_amd.optim import FusedAdam
 
     timer = KernelTimer()
+    F_ = None
     if not args.no_kernel_timing:
         install_timers(timer)
+        import nerf_pl_amd.functions as F_
 
     if args.config == "eval":
         wl = wl_eval(args, dev, rank)
@@ -684,6 +711,8 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         timer.events = {}
+        if F_ is not None:
+            F_.ACTIVE_LOG = []
         timer.enabled = True
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -721,7 +750,7 @@ def main():
                 ks[dom]["share_of_step"] = ks[dom]["total_ms"] / (ms * steps)
                 # the MLP stage (every fused MLP launch: forward, data and weight
                 # gradients) against the fp32 MFMA peak -- the north star's ratio
-                fl = sum(KERNEL_FLOP[k] * n for k in roofs for *_, n in timer.events[k])
+                fl = sum(KERNEL_FLOP[k] * active_samples(ev) for k in roofs for ev in timer.events[k])
                 t = sum(ks[k]["total_ms"] for k in roofs)
                 tf_ = fl / (t * 1e-3) / 1e12
                 stage = dict(kernels=sorted(roofs), ms_per_step=round(t / steps, 4),
@@ -737,6 +766,20 @@ def main():
     math_main = _math()
     ks, roof, roofs, stage = rooflines(math_main, ms, args.steps)
 
+    # the split arithmetics' backward skips the samples whose output gradient
+    # is exactly zero (nr_active_samples): the share it worked on, per launch
+    # size (coarse / fine pass), over the timed steps
+    from nerf_pl_amd import functions as _functions
+    backward_blocks = dict(skip_zero_gradient_samples=bool(_functions.ACTIVE_SAMPLES
+                                                           and math_main in ("f16x3", "bf16x6")))
+    for k in ("mlp_bwd_dgrad", "mlp_bwd_dgrad_sigma"):
+        evs = timer.events.get(k, [])
+        if evs and any(ev[3] is not None for ev in evs):
+            by_n = {}
+            for ev in evs:
+                by_n.setdefault(ev[2], []).append(active_samples(ev) / ev[2])
+            backward_blocks[k] = {f"samples_{n}": round(sum(v) / len(v), 4)
+                                  for n, v in sorted(by_n.items())}
     # exact-fp32 leg: the same workload on v_mfma_f32_32x32x2_f32 (fp32
     # products, no operand splitting) -- its own roofline against the fp32
     # MFMA peak, next to the default arithmetic's
@@ -809,6 +852,7 @@ def main():
             "rooflines": roofs,
             "mlp_stage": stage,
             "fp32_leg": fp32_leg,
+            "backward_samples": backward_blocks,
             "cpu_baseline": cpu,
             "cpu_baseline_1thread": cpu1,
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv

@@ -29,12 +29,56 @@ def seg_zero(buf, off, width, nb):
     return float((x == 0).float().mean())
 
 
+def block_stats(g_out):
+    """fractions of samples / 32-sample blocks / 128-sample workgroups whose
+    whole output gradient (d rgb, d sigma) is exactly zero"""
+    n = g_out.shape[0]
+    z = (g_out != 0).any(1)
+    out = {"samples": n, "zero_grad_samples": round(1 - float(z.float().mean()), 4)}
+    for k, name in ((32, "zero_grad_blocks32"), (128, "zero_grad_groups128")):
+        m = n // k * k
+        out[name] = round(1 - float(z[:m].view(-1, k).any(1).float().mean()), 4)
+    return out
+
+
+def bench_mode(out_path):
+    """the bench's own cfg2 training step (seeded default init), a few steps"""
+    import bench
+    from nerf_pl_amd import functions
+    from nerf_pl_amd.optim import FusedAdam
+    args = bench.parse_args_for(["--config", "cfg2"]) if hasattr(bench, "parse_args_for") else None
+    if args is None:
+        sys.argv = ["bench.py"]
+        args = bench.parse()
+    dev = torch.device("cuda", 0)
+    wl = bench.wl_nerf_train(args, dev, 0, ndc=False)
+    params = [p for m in wl["models"] for p in m.parameters()]
+    opt = FusedAdam(params, lr=5e-4, eps=1e-8)
+    res = {"workload": wl["workload"], "steps": []}
+    for it in range(6):
+        functions._DEBUG.clear()
+        loss = wl["step"]()
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        g = functions._DEBUG["g_outs"]      # fine backward first, then coarse
+        row = {"step": it, "fine": block_stats(g[0]), "coarse": block_stats(g[1])}
+        res["steps"].append(row)
+        print(json.dumps(row), flush=True)
+    if out_path:
+        with open(out_path, "w") as f:
+            json.dump(res, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--weights", default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--bench", action="store_true", help="the bench's cfg2 step instead")
     args = ap.parse_args()
     assert os.environ.get("NERF_PL_AMD_DEBUG") == "1", "run with NERF_PL_AMD_DEBUG=1"
+    if args.bench:
+        return bench_mode(args.out)
     import psnr_compare as pc
     from nerf_pl_amd import Embedding, NeRF, functions, ops, render_rays
     dev = torch.device("cuda", 0)
@@ -62,6 +106,7 @@ def main():
         nb = ops.n_blocks(n)
         save, gws = d["save"], d["grad_ws"]
         r = {"samples": n}
+        r.update(block_stats(d["g_out"][:n]))
         r["pe"] = seg_zero(save, 0, 64, nb)
         for l in range(8):
             r[f"h{l + 1}"] = seg_zero(save, (64 + l * 256) * W32 * nb, 256, nb)

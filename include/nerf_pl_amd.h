@@ -157,6 +157,47 @@ int nr_wgrad_sigma_h3(const float* save, const float* grad_ws, int64_t n, float*
 int nr_wgrad_sigma_b1(const float* save, const float* grad_ws, int64_t n, float* workspace,
                       float* grad_flat, void* stream);
 
+/* Zero-gradient samples (the training backward of rendering.py:169-176 under
+ * autograd, train.py:107-111).  A sample whose output gradient g_out row
+ * (d rgb, d sigma) is exactly zero -- sigma clamped by the ReLU (alpha = 0:
+ * weight 0 and no sigma gradient) or a transmittance underflowed behind an
+ * opaque surface -- adds exactly zero to every layer's dz and weight-gradient
+ * sum.  nr_active_samples writes the indices of the other samples (a nonzero
+ * or NaN entry in their row), ascending, to samples[0 .. m) (n int32), m to
+ * *count (device memory, no host sync); scratch: nr_active_scratch_ints(n)
+ * int32.  The *_active data- and weight-gradient entry points (plain twins'
+ * arguments plus samples / count) then run over the m listed samples packed
+ * densely: grad_ws holds position q's rows (q < m, sample samples[q]), so it
+ * feeds only nr_wgrad*_active with the same list, which gathers the saved
+ * activations of samples[q]; the weight gradients equal the plain entry
+ * points' up to the order of the split-K partial sums (a fixed order:
+ * reproducible).  Split arithmetics (x3 = bf16x6, h3 = f16x3) only. */
+int64_t nr_active_scratch_ints(int64_t n);
+int nr_active_samples(const float* g_out, int64_t n, int32_t* samples, int32_t* count,
+                      int32_t* scratch, void* stream);
+int nr_mlp_bwd_active_x3(const void* packed_bwd, const float* head, const float* out,
+                         const float* g_out, const float* save, int64_t n, float* grad_ws,
+                         const int32_t* samples, const int32_t* count, void* stream);
+int nr_mlp_bwd_active_h3(const void* packed_bwd, const float* head, const float* out,
+                         const float* g_out, const float* save, int64_t n, float* grad_ws,
+                         const int32_t* samples, const int32_t* count, void* stream);
+int nr_mlp_bwd_sigma_active_x3(const void* packed_bwd, const float* head, const float* out,
+                               const float* g_out, const float* save, int64_t n, float* grad_ws,
+                               const int32_t* samples, const int32_t* count, void* stream);
+int nr_mlp_bwd_sigma_active_h3(const void* packed_bwd, const float* head, const float* out,
+                               const float* g_out, const float* save, int64_t n, float* grad_ws,
+                               const int32_t* samples, const int32_t* count, void* stream);
+int nr_wgrad_active_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                       float* grad_flat, const int32_t* samples, const int32_t* count, void* stream);
+int nr_wgrad_active_h3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                       float* grad_flat, const int32_t* samples, const int32_t* count, void* stream);
+int nr_wgrad_sigma_active_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                             float* grad_flat, const int32_t* samples, const int32_t* count,
+                             void* stream);
+int nr_wgrad_sigma_active_h3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                             float* grad_flat, const int32_t* samples, const int32_t* count,
+                             void* stream);
+
 /* Dense sigma query (extract_color_mesh.py:114-137, the marching-cubes grid):
  * sigma_out (n) = NeRF sigma head at points pts (n,3) -- the sigma-only fused
  * kernel with the positional encoding computed in-kernel (sigma does not

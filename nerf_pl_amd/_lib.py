@@ -51,6 +51,16 @@ SIGNATURES = {
     "nr_mlp_bwd_sigma_b1": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_b1": [_p, _p, _i64, _p, _p, _p],
     "nr_wgrad_sigma_b1": [_p, _p, _i64, _p, _p, _p],
+    "nr_active_samples": [_p, _i64, _p, _p, _p, _p],
+    "nr_active_scratch_ints": [_i64],
+    "nr_mlp_bwd_active_x3": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_mlp_bwd_active_h3": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_mlp_bwd_sigma_active_x3": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_mlp_bwd_sigma_active_h3": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_wgrad_active_x3": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_wgrad_active_h3": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_wgrad_sigma_active_x3": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_wgrad_sigma_active_h3": [_p, _p, _i64, _p, _p, _p, _p, _p],
     "nr_mlp_bwd": [_p, _p, _p, _p, _p, _i64, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
     "nr_sm_workspace_bytes": [_i64, _i64],
@@ -85,7 +95,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"nr_layout_query": _i64, "nr_adam_max_tensors": _i, "nr_fwd3_packed_bytes": _i64,
              "nr_fwd3_packed_bytes_h3": _i64, "nr_fwd3_packed_bytes_b1": _i64,
-             "nr_wgrad_workspace_bytes": _i64,
+             "nr_wgrad_workspace_bytes": _i64, "nr_active_scratch_ints": _i64,
              "nr_sm_workspace_bytes": _i64, "nr_last_error": ctypes.c_char_p}
 
 _lib = None

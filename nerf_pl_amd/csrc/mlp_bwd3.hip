@@ -151,13 +151,19 @@ struct Bwd3Args {
     int n;
     float* grad;
     float* stats;    // f16x3: per-wave maxima [NR_STAT_SEGS][nb] (layout.h, in the save buffer)
+    // optional (active.hip): the ascending list of the samples with a nonzero
+    // output gradient and its length m; the chain then runs over them packed
+    // densely -- position q < m holds sample slist[q] -- and every output
+    // (dz, dhead, stats) is indexed by position
+    const int32_t* slist; const int32_t* scount;
 };
 
 // SO: the sigma-only graph (rendering_shadows.py:167, sigma_only=True): no rgb
 // head, dir layer or xyz_encoding_final, so the chain starts at d h8 =
 // W_sigma^T dsigma and the ring streams the transposed weights from layer 8
 // on (the packed buffer from group kL8T, the group indices shifted by kB)
-template <bool SO>
+// GA: over the packed sample list a.slist (the *_active entry points)
+template <bool SO, bool GA>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     constexpr int kB = SO ? kL8T : 0;      // first k-group streamed
     constexpr int QE = kQ - kB;            // groups streamed
@@ -165,9 +171,23 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4;
-    const int blk = blockIdx.x * kWaves + wave;
     const int nreal = (a.n + 31) / 32;
     const int nb = (int)nr_blocks_pad(a.n);     // segment stride; dead waves write padding
+    const int blk = blockIdx.x * kWaves + wave;   // block of (packed) positions
+    // m: samples (positions) the chain runs over.  With a sample list,
+    // workgroups past its end only zero their stats slots: the weight
+    // gradient reads positions < m only
+    int m = a.n;
+    if constexpr (GA) {
+        m = __builtin_amdgcn_readfirstlane(*a.scount);
+        if ((int)blockIdx.x * kWaves * 32 >= m) {
+            if constexpr (NR_F16) {
+#pragma unroll 1
+                for (int l = 0; l < NR_STAT_SEGS; ++l) report_max(0.f, a.stats + l * nb + blk, lane);
+            }
+            return;
+        }
+    }
     const bool live = blk < nreal;
     const char* PB = a.packed;
     const float* SV = a.save;
@@ -176,7 +196,17 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     // ReLU mask words (9 layers) and the head block by LDS-DMA, issued before
     // the ring so the ring's counted waits cover them
     uint4* smask = reinterpret_cast<uint4*>(smem + kRingBytes) + wave * NR_MASK_LAYERS * 64;
-    {
+    // the samples of this lane's columns (sample tiles S = 0, 1): position
+    // 32 blk + 16 S + (lane & 15), sample slist[position] with a list
+    int sidx[2];
+    bool valid[2];
+#pragma unroll
+    for (int S = 0; S < 2; ++S) {
+        const int q = blk * 32 + 16 * S + (lane & 15);
+        valid[S] = q < m;
+        sidx[S] = !valid[S] ? (GA ? 0 : a.n - 1) : (GA ? a.slist[q] : q);
+    }
+    if constexpr (!GA) {
         const uint4* gm = reinterpret_cast<const uint4*>(SV + nr_sv_mask(nb)) +
                           (size_t)blk * NR_MASK_LAYERS * 64 + lane;
 #pragma unroll
@@ -184,6 +214,31 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
             __builtin_amdgcn_global_load_lds(
                 (const void*)(gm + l * 64),
                 (__attribute__((address_space(3))) void*)(smask + l * 64), 16, 0, 0);
+    } else {
+        // gather: sample s = 32 b + 16 S' + c' keeps its ReLU bits in lane
+        // 16 g + c' of block b, word k bits 8 i + 4 S' + r (x3.h mask_bits);
+        // repack them at this lane's tile S (a wave reads only its own slots)
+        const uint4* gm = reinterpret_cast<const uint4*>(SV + nr_sv_mask(nb));
+        const uint4* src[2];
+        int sh[2];
+#pragma unroll
+        for (int S = 0; S < 2; ++S) {
+            const int s = sidx[S];
+            src[S] = gm + (size_t)(s >> 5) * NR_MASK_LAYERS * 64 + 16 * g + (s & 15);
+            sh[S] = 4 * ((s >> 4) & 1);
+        }
+#pragma unroll
+        for (int l = 0; l < NR_MASK_LAYERS; ++l) {
+            const uint4 w0 = src[0][l * 64], w1 = src[1][l * 64];
+            auto mix = [&](uint32_t x0, uint32_t x1, int S0ok, int S1ok) {
+                return (S0ok ? ((x0 >> sh[0]) & 0x0F0F0F0Fu) : 0u) |
+                       (S1ok ? (((x1 >> sh[1]) & 0x0F0F0F0Fu) << 4) : 0u);
+            };
+            smask[l * 64 + lane] = make_uint4(mix(w0.x, w1.x, valid[0], valid[1]),
+                                              mix(w0.y, w1.y, valid[0], valid[1]),
+                                              mix(w0.z, w1.z, valid[0], valid[1]),
+                                              mix(w0.w, w1.w, valid[0], valid[1]));
+        }
     }
     float* Hs = reinterpret_cast<float*>(smem + kRingBytes + kMaskBytes);
     {
@@ -196,14 +251,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     const Dma dma = make_dma(PB + BwdTab::off(kB), BwdTab::off(QE), smem, wave, lane);
     prologue<BwdTab, QE>(dma);
     f32x4 go[2], yo[2];
-    bool valid[2];
 #pragma unroll
     for (int S = 0; S < 2; ++S) {
-        const int s_raw = blk * 32 + 16 * S + (lane & 15);
-        valid[S] = s_raw < a.n;
-        const int s = valid[S] ? s_raw : a.n - 1;
-        go[S] = *reinterpret_cast<const f32x4*>(a.g_out + (size_t)s * 4);
-        yo[S] = *reinterpret_cast<const f32x4*>(a.out + (size_t)s * 4);
+        go[S] = *reinterpret_cast<const f32x4*>(a.g_out + (size_t)sidx[S] * 4);
+        yo[S] = *reinterpret_cast<const f32x4*>(a.out + (size_t)sidx[S] * 4);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // masks, head (and the prologue) landed
     __builtin_amdgcn_s_barrier();                       // head visible to every wave
@@ -445,7 +496,8 @@ NR_API int NR_X3_NAME(nr_pack_bwd)(const float* flat, const int32_t* map, int64_
 namespace {
 int bwd3_launch(const char* name, bool sigma_only, const void* packed_bwd, const float* head,
                 const float* out, const float* g_out, const float* save, int64_t n,
-                float* grad_ws, void* stream) {
+                float* grad_ws, void* stream, const int32_t* slist = nullptr,
+                const int32_t* scount = nullptr) {
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "%s: n out of range", name);
     if (n == 0) return 0;
     NR_REQUIRE(packed_bwd && head && out && g_out && save && grad_ws, "%s: null pointer", name);
@@ -454,10 +506,21 @@ int bwd3_launch(const char* name, bool sigma_only, const void* packed_bwd, const
                "%s: buffers must be 16-byte aligned", name);
     float* stats = const_cast<float*>(save) + nr_sv_stats(nr_blocks_pad(n)) + NR_STATS;
     Bwd3Args a{reinterpret_cast<const char*>(packed_bwd), head, out, g_out, save, (int)n, grad_ws,
-               stats};
+               stats, slist, scount};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
-    if (sigma_only) mlp_bwd3_kernel<true><<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
-    else mlp_bwd3_kernel<false><<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
+    hipStream_t st = (hipStream_t)stream;
+#if NR_BF1     // no sample lists for the bf16 variant
+    if (sigma_only) mlp_bwd3_kernel<true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else mlp_bwd3_kernel<false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+#else
+    if (slist) {
+        if (sigma_only) mlp_bwd3_kernel<true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_bwd3_kernel<false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+    } else {
+        if (sigma_only) mlp_bwd3_kernel<true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_bwd3_kernel<false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+    }
+#endif
     NR_LAUNCH_CHECK(name);
     return 0;
 }
@@ -478,3 +541,26 @@ NR_API int NR_X3_NAME(nr_mlp_bwd_sigma)(const void* packed_bwd, const float* hea
     return bwd3_launch("nr_mlp_bwd_sigma_x3", true, packed_bwd, head, out, g_out, save, n,
                        grad_ws, stream);
 }
+
+#if !NR_BF1
+// the same over the samples nr_active_samples listed (samples / count on the
+// device), packed: grad_ws holds position q's rows at q -- only the matching
+// nr_wgrad*_active entry point (same list) may consume it
+NR_API int NR_X3_NAME(nr_mlp_bwd_active)(const void* packed_bwd, const float* head,
+                                         const float* out, const float* g_out, const float* save,
+                                         int64_t n, float* grad_ws, const int32_t* samples,
+                                         const int32_t* count, void* stream) {
+    NR_REQUIRE(samples && count, "nr_mlp_bwd_active: null sample list");
+    return bwd3_launch("nr_mlp_bwd_active", false, packed_bwd, head, out, g_out, save, n, grad_ws,
+                       stream, samples, count);
+}
+NR_API int NR_X3_NAME(nr_mlp_bwd_sigma_active)(const void* packed_bwd, const float* head,
+                                               const float* out, const float* g_out,
+                                               const float* save, int64_t n, float* grad_ws,
+                                               const int32_t* samples, const int32_t* count,
+                                               void* stream) {
+    NR_REQUIRE(samples && count, "nr_mlp_bwd_sigma_active: null sample list");
+    return bwd3_launch("nr_mlp_bwd_sigma_active", true, packed_bwd, head, out, g_out, save, n,
+                       grad_ws, stream, samples, count);
+}
+#endif

@@ -97,7 +97,22 @@ struct WgArgs {
     float* slab;
     bool x3;             // segments in the bf16x6 pipeline's N16 layout (x3.h)
     const float* stats;  // f16x3: max |gradient| per segment (mlp_bwd3.hip), else null
+    // optional (active.hip, split arithmetics' wgrad3_body only): the ascending
+    // list of the samples with a nonzero output gradient and its length m on
+    // the device.  The gradient segments (mlp_bwd3.hip *_active) then hold
+    // position q's rows at q; the split-K ranges cover the ceil(m / 32) blocks
+    // of positions, and the input operands are gathered from sample slist[q]
+    const int32_t* slist; const int32_t* scount;
 };
+
+// samples (positions) a launch works on
+__device__ __forceinline__ int wg_m(const WgArgs& a) {
+    return a.slist ? __builtin_amdgcn_readfirstlane(*a.scount) : a.n;
+}
+// blocks of positions a launch's split-K ranges cover
+__device__ __forceinline__ int wg_nact(const WgArgs& a) {
+    return a.slist ? (wg_m(a) + 31) / 32 : a.nb;
+}
 
 // f16x3: the gradient operand of a task is scaled by 2^(kWT - e(max |dz|)) so
 // its largest element sits in [2^kWT, 2^(kWT+1)) < 65504; the input operand
@@ -270,8 +285,9 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
     const int c = blockIdx.x - a.wg_start[t];
     const WgTask& T = a.task[t];
-    const int b0 = (int)((int64_t)c * a.nb / T.G);
-    const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
+    const int nact = wg_nact(a);
+    const int b0 = (int)((int64_t)c * nact / T.G);
+    const int b1 = (int)((int64_t)(c + 1) * nact / T.G);
     float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
     // task shapes (see nr_wgrad's task list); wave-uniform
     // (WM, WN) = wave grid over the task's output (<= 8 waves; 128 accumulators max)
@@ -392,6 +408,19 @@ struct Stager {
 #endif
         }
     }
+    // the same two samples gathered: sample s of the list (s0, s1) sits at
+    // block s / 32, half-block (s / 16) & 1, lane column s & 15
+    __device__ __forceinline__ void load_g(const float* base, int s0, int s1) {
+        static_assert(KIND != SEG_HEAD, "head segments are gradients (packed by position)");
+#if NR_BF1
+        (void)base; (void)s0; (void)s1;
+#else
+        constexpr int F4 = Geo3<KIND, W>::CHUNKS * 64;
+        const f32x4* b = reinterpret_cast<const f32x4*>(base);
+        v0 = ld_seg(b + (size_t)(s0 >> 5) * F4 + Geo3<KIND, W>::f4(k, h, (s0 >> 4) & 1, s0 & 15));
+        v1 = ld_seg(b + (size_t)(s1 >> 5) * F4 + Geo3<KIND, W>::f4(k, h, (s1 >> 4) & 1, s1 & 15));
+#endif
+    }
     // split + store column e of this thread's chunk into an operand image
     // (values times sc, a power of two); samples >= nval become 0; adds the two
     // samples' unscaled sum (bias) to s
@@ -433,6 +462,12 @@ struct ThinStager {
 #endif
         v = ld_seg(reinterpret_cast<const x3::f32x2*>(base + f));
     }
+    // the same pair of sample s (gathered, see Stager::load_g)
+    __device__ __forceinline__ void load_g(const float* base, int s) {
+        const size_t f = 4 * ((size_t)(s >> 5) * (W / 8) * 64 + ((c >> 4) * 2 + ((s >> 4) & 1)) * 64 +
+                              16 * ((c & 15) >> 2) + (s & 15)) + (c & 3);
+        v = ld_seg(reinterpret_cast<const x3::f32x2*>(base + f));
+    }
     // split + store this thread's pair (times sc); s0/s1 += the unscaled values
     __device__ __forceinline__ void store(char* img, int nval, float& s0, float& s1, float sc) {
         if (!act) return;
@@ -471,8 +506,8 @@ __device__ __forceinline__ x3::Pieces frag(const char* q, int plane) {
 // 4-row head: extra output XW x N); its XWM x XWN wave grid covers the extra
 // output (grids smaller than 8 waves are computed twice, written once) and the
 // result goes to the partner task's slab `xslab`.
-template <int KA, int WA, int KB, int WB, int WM, int WN, int XK = -1, int XW = 0, int XS = 0,
-          int XWM = 1, int XWN = 1>
+template <bool GA, int KA, int WA, int KB, int WB, int WM, int WN, int XK = -1, int XW = 0,
+          int XS = 0, int XWM = 1, int XWN = 1>
 __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, int b0, int b1,
                                             char* lds, float* __restrict__ slab,
                                             float* __restrict__ xslab = nullptr) {
@@ -535,17 +570,47 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
     // nobody reads again
     const int blast = b1 > b0 ? b1 - 1 : b0;
     const float* xbase = HX ? (XS ? a.task[T.fuse].a.base : a.task[T.fuse].b.base) : nullptr;
+    // [b0, b1) are blocks of positions.  With a sample list (a.slist) the
+    // gradient operands are packed by position and the input operands are
+    // gathered: position q holds sample slist[q] (positions past m load
+    // sample 0 and stage zeros).  Each register set holds the list entries of
+    // the stage it loads next, fetched when its previous stage was loaded
+    const int m = wg_m(a);
+    constexpr bool gat = GA;
+    auto sample_at = [&](int st, int j) {   // positions past m: sample 0 (staged as zeros)
+        const int q = min(b0 + (st >> 1), blast) * 32 + 16 * (st & 1) + j;
+        return q < m ? a.slist[q] : 0;
+    };
+    constexpr bool XIN = HX && XS == 0;    // the extra operand is an input segment
+    int ns[2][2] = {{0, 0}, {0, 0}}, nx[2] = {0, 0};
+    // B operand (input segment): this thread's samples 2 jp, 2 jp + 1; the
+    // extra input operand: sample j of its ThinStager
+    auto fetch = [&](int set, int st) {
+        if constexpr (!gat) return;
+        ns[set][0] = sample_at(st, 2 * sb[set].jp);
+        ns[set][1] = sample_at(st, 2 * sb[set].jp + 1);
+        if constexpr (XIN) nx[set] = sample_at(st, sx[set].j);
+    };
+    fetch(0, 0);
+    fetch(1, 1);
     auto load = [&](int set, int st) {
         if (NR_W3_DBG == 2 && st > 1) return;
         const int blk = min(b0 + (st >> 1), blast), hb = st & 1;
         sa[set].load(T.a.base, blk, hb);
-        sb[set].load(T.b.base, blk, hb);
-        if constexpr (HX) sx[set].load(xbase, blk, hb);
+        if constexpr (gat) {
+            sb[set].load_g(T.b.base, ns[set][0], ns[set][1]);
+            if constexpr (XIN) sx[set].load_g(xbase, nx[set]);
+            else if constexpr (HX) sx[set].load(xbase, blk, hb);
+            fetch(set, st + 2);
+        } else {
+            sb[set].load(T.b.base, blk, hb);
+            if constexpr (HX) sx[set].load(xbase, blk, hb);
+        }
     };
     const float sca = task_scale(a, T);
     const float scx = HX && XS ? task_scale(a, a.task[T.fuse]) : 1.f;
     auto store = [&](int set, int buf, int st) {
-        const int nval = st < nst ? a.n - (b0 + (st >> 1)) * 32 - 16 * (st & 1) : 0;
+        const int nval = st < nst ? m - (b0 + (st >> 1)) * 32 - 16 * (st & 1) : 0;
         float sdummy = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -566,7 +631,7 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
     // LDS-store work overlaps the MFMAs in flight instead of idling both waves
     // of a SIMD at the same time; the extra operand's 4 units follow its MFMAs
     auto compute_store = [&](int buf, int set, int st_next) {
-        const int nval = st_next < nst ? a.n - (b0 + (st_next >> 1)) * 32 - 16 * (st_next & 1) : 0;
+        const int nval = st_next < nst ? m - (b0 + (st_next >> 1)) * 32 - 16 * (st_next & 1) : 0;
         char* ia = lds + (buf ^ 1) * kBufB;
         char* ib = ia + kOpnd;
         char* ix = ia + 2 * kOpnd;
@@ -983,6 +1048,8 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
 }
 #endif  // NR_BF1
 
+// GA: the packed sample list a.slist (the *_active entry points)
+template <bool GA>
 __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
 #if NR_BF1
     __shared__ __attribute__((aligned(16))) char lds[b1::kLds > w3::kLds ? b1::kLds : w3::kLds];
@@ -994,8 +1061,9 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
     while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
     const int c = blockIdx.x - a.wg_start[t];
     const WgTask& T = a.task[t];
-    const int b0 = (int)((int64_t)c * a.nb / T.G);
-    const int b1 = (int)((int64_t)(c + 1) * a.nb / T.G);
+    const int nact = wg_nact(a);
+    const int b0 = (int)((int64_t)c * nact / T.G);
+    const int b1 = (int)((int64_t)(c + 1) * nact / T.G);
     float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
     const int fu = __builtin_amdgcn_readfirstlane(T.fuse);
     if constexpr (kFuse) if (fu >= 0) {
@@ -1016,17 +1084,17 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
         switch (__builtin_amdgcn_readfirstlane(T.id)) {
 #if NR_WGRAD_FUSE_MASK & 1
             case 5:    // DZ(4) x [H(3) | PE]: xyz_encoding_5 (skip layer)
-                wgrad3_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_PE, 64, 0, NR_WG_PE_WM, 8 / NR_WG_PE_WM>(
+                wgrad3_body<GA, SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_PE, 64, 0, NR_WG_PE_WM, 8 / NR_WG_PE_WM>(
                     a, T, b0, b1, lds, slab, xslab); break;
 #endif
 #if NR_WGRAD_FUSE_MASK & 2
             case 9:    // [DZ(8) | head] x H(7): xyz_encoding_final and sigma
-                wgrad3_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_HEAD, 4, 1, 1, 8>(
+                wgrad3_body<GA, SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_HEAD, 4, 1, 1, 8>(
                     a, T, b0, b1, lds, slab, xslab); break;
 #endif
 #if NR_WGRAD_FUSE_MASK & 4
             case 10:   // dz_dir x [feat | dir PE]: dir_encoding
-                wgrad3_body<SEG_ACC, 128, SEG_ACC, 256, 2, 4, SEG_DPE, 32, 0, 4, 1>(
+                wgrad3_body<GA, SEG_ACC, 128, SEG_ACC, 256, 2, 4, SEG_DPE, 32, 0, 4, 1>(
                     a, T, b0, b1, lds, slab, xslab); break;
 #endif
         }
@@ -1051,17 +1119,17 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
 #endif
     switch (__builtin_amdgcn_readfirstlane(T.id)) {
         case 0: case 4:
-            wgrad3_body<SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
         case 10:
-            wgrad3_body<SEG_ACC, 128, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, SEG_ACC, 128, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
         case 11:
-            wgrad3_body<SEG_ACC, 128, SEG_DPE, 32, 4, 1>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, SEG_ACC, 128, SEG_DPE, 32, 4, 1>(a, T, b0, b1, lds, slab); break;
         case 12:
-            wgrad3_body<SEG_HEAD, 4, SEG_ACC, 256, 1, 8>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, SEG_HEAD, 4, SEG_ACC, 256, 1, 8>(a, T, b0, b1, lds, slab); break;
         case 13:
-            wgrad3_body<SEG_HEAD, 4, SEG_ACC, 128, 1, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, SEG_HEAD, 4, SEG_ACC, 128, 1, 4>(a, T, b0, b1, lds, slab); break;
         default:
-            wgrad3_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, SEG_ACC, 256, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
     }
 }
 
@@ -1176,7 +1244,8 @@ NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
 
 namespace {
 int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_ws, int64_t n,
-                 float* workspace, float* grad_flat, void* stream) {
+                 float* workspace, float* grad_flat, void* stream,
+                 const int32_t* slist = nullptr, const int32_t* scount = nullptr) {
     const char* name = sigma_only ? "nr_wgrad_sigma" : "nr_wgrad";
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "%s: n out of range", name);
     NR_REQUIRE(save && grad_ws && workspace && grad_flat, "%s: null pointer", name);
@@ -1291,14 +1360,18 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     a.slab = workspace;
     a.x3 = x3;
     a.stats = NR_F16 ? SV + nr_sv_stats(nbp) : nullptr;
+    a.slist = slist;
+    a.scount = scount;
 #if NR_F16
     stats_reduce_kernel<<<NR_STAT_SEGS, kStatT, 0, st>>>(SV + nr_sv_stats(nbp), (int)nbp);
     NR_LAUNCH_CHECK("nr_wgrad_stats");
-    wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    if (slist) wgrad3_kernel<true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else wgrad3_kernel<false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #elif NR_BF1
-    wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    wgrad3_kernel<false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #else
-    if (x3) wgrad3_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    if (x3 && slist) wgrad3_kernel<true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (x3) wgrad3_kernel<false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else wgrad_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #endif
     NR_LAUNCH_CHECK("nr_wgrad");
@@ -1327,3 +1400,22 @@ NR_API int NR_X3_NAME(nr_wgrad_sigma)(const float* save, const float* grad_ws, i
                              float* workspace, float* grad_flat, void* stream) {
     return wgrad_launch(true, true, save, grad_ws, n, workspace, grad_flat, stream);
 }
+
+#if !NR_BF1
+// over the samples nr_active_samples listed (after nr_mlp_bwd*_active with the
+// same list); the other samples' output gradients are exactly zero, so the
+// sums are those of nr_wgrad* up to the order of the split-K partial sums
+NR_API int NR_X3_NAME(nr_wgrad_active)(const float* save, const float* grad_ws, int64_t n,
+                                       float* workspace, float* grad_flat, const int32_t* samples,
+                                       const int32_t* count, void* stream) {
+    NR_REQUIRE(samples && count, "nr_wgrad_active: null sample list");
+    return wgrad_launch(true, false, save, grad_ws, n, workspace, grad_flat, stream, samples, count);
+}
+NR_API int NR_X3_NAME(nr_wgrad_sigma_active)(const float* save, const float* grad_ws, int64_t n,
+                                             float* workspace, float* grad_flat,
+                                             const int32_t* samples, const int32_t* count,
+                                             void* stream) {
+    NR_REQUIRE(samples && count, "nr_wgrad_sigma_active: null sample list");
+    return wgrad_launch(true, true, save, grad_ws, n, workspace, grad_flat, stream, samples, count);
+}
+#endif

@@ -38,6 +38,14 @@ def _wgrad_workspace(device_index: int, stream: int = 0) -> torch.Tensor:
 # on the full kernels with a zero rgb gradient -- the A/B reference of the tests)
 SIGMA_TRAIN_KERNELS = os.environ.get("NERF_PL_AMD_SIGMA_TRAIN", "1") != "0"
 
+# the split arithmetics' backward works on the samples with a nonzero output
+# gradient only (nr_active_samples; exact: the others add zeros to every sum),
+# packed densely.  NERF_PL_AMD_ACTIVE_SAMPLES=0: every sample (the A/B reference)
+ACTIVE_SAMPLES = os.environ.get("NERF_PL_AMD_ACTIVE_SAMPLES", "1") != "0"
+# bench.py's kernel timer: a list every backward appends its (sample list
+# buffer, index of its length) to, so the rooflines count the samples worked on
+ACTIVE_LOG = None
+
 # NERF_PL_AMD_DEBUG=1 keeps the last backward's buffers here (dev/ scripts)
 _DEBUG = {} if os.environ.get("NERF_PL_AMD_DEBUG") == "1" else None
 
@@ -85,15 +93,27 @@ class _FusedMLP(torch.autograd.Function):
         grad_ws = torch.empty(ops.n_blocks(n) * ops.GRAD_PER_BLOCK, device=dev)
         g_out = g_out.contiguous()
         sfx = "_sigma" if ctx.so_kernels else ""
+        st = stream_of(dev)
+        active = ()
+        if ACTIVE_SAMPLES and ops.arith_of(packed_b) in ("f16x3", "bf16x6"):
+            # the samples with a nonzero output gradient, ascending (int32 [0, n)),
+            # their count ([n]) and the compaction's scratch
+            sl = torch.empty(n + 1 + 2 * ((n + 31) // 32), dtype=torch.int32, device=dev)
+            call("nr_active_samples", g_out.data_ptr(), n, sl.data_ptr(), sl.data_ptr() + 4 * n,
+                 sl.data_ptr() + 4 * (n + 1), st)
+            active = (sl.data_ptr(), sl.data_ptr() + 4 * n)
+            if ACTIVE_LOG is not None:
+                ACTIVE_LOG.append((sl, n))
+            sfx += "_active"
         call(ops.entry("nr_mlp_bwd" + sfx, packed_b), packed_b.data_ptr(), ops.head_ptr(packed_f),
-             out.data_ptr(), g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(),
-             stream_of(dev))
+             out.data_ptr(), g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), *active, st)
         gflat = torch.empty(packing.N_PARAMS, device=dev)
-        ws = _wgrad_workspace(dev.index, int(stream_of(dev)))
+        ws = _wgrad_workspace(dev.index, int(st))
         call(ops.entry("nr_wgrad" + sfx, packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
-             ws.data_ptr(), gflat.data_ptr(), stream_of(dev))
+             ws.data_ptr(), gflat.data_ptr(), *active, st)
         if _DEBUG is not None:
             _DEBUG.update(save=save, grad_ws=grad_ws, g_out=g_out, gflat=gflat, n=n)
+            _DEBUG.setdefault("g_outs", []).append(g_out)
         grads, off = [], 0
         for name, shp in _SHAPES:
             k = 1

@@ -33,10 +33,18 @@ def _cases():
                   (f"nr_mlp_bwd_sigma{sfx}", [N, N, N, N, N, 5, N, N], NR_EINVAL),
                   (f"nr_wgrad_sigma{sfx}", [N, N, -1, N, N, N], NR_EINVAL),
                   (f"nr_wgrad_sigma{sfx}", [N, N, 5, N, N, N], NR_EINVAL)]
+        if sfx in ("_x3", "_h3"):     # zero-gradient sample lists (split arithmetics)
+            for so in ("", "_sigma"):
+                c += [(f"nr_mlp_bwd{so}_active{sfx}", [N, N, N, N, N, -1, N, N, N, N], NR_EINVAL),
+                      (f"nr_mlp_bwd{so}_active{sfx}", [N, N, N, N, N, 5, N, N, N, N], NR_EINVAL),
+                      (f"nr_wgrad{so}_active{sfx}", [N, N, -1, N, N, N, N, N], NR_EINVAL),
+                      (f"nr_wgrad{so}_active{sfx}", [N, N, 5, N, N, N, N, N], NR_EINVAL)]
         if sfx:
             c += [(f"nr_pack{sfx}", [N, N, -1, N, N, N], NR_EINVAL),
                   (f"nr_pack_bwd{sfx}", [N, N, -1, N, N], NR_EINVAL)]
     c += [
+        ("nr_active_samples", [N, -1, N, N, N, N], NR_EINVAL),
+        ("nr_active_samples", [N, 5, N, N, N, N], NR_EINVAL),
         ("nr_pack", [N, N, -1, N, N], NR_EINVAL),
         ("nr_pack", [N, N, 0, N, N], 0),
         ("nr_pack", [N, N, 7, N, N], NR_EINVAL),
