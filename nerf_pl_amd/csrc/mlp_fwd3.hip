@@ -127,15 +127,17 @@ __device__ __forceinline__ void dir_gather(float (&d)[8], const float* __restric
     d[7] = 0.f;
 }
 
-// slot values 4u .. 4u+3 (u = 2s + jh of the lane's 8-slot cells) -> the N16
-// saved layout: slots 32s + 8g + 4jh = tile 2s + (g >> 1), group 2(g & 1) + jh
+// slot values 4u .. 4u+3 (u = 2s + jh of the lane's 8-slot cells) -> the
+// saved slots 32s + 8g + 4jh = tile 2s + (g >> 1), group 2(g & 1) + jh: N16
+// (bf16) or the sample-major rows of W slots (x3.h store_row)
+template <int W>
 __device__ __forceinline__ void store_pe4(const float* v, int s, int jh, int S, int g,
                                           float* __restrict__ blk, int lane) {
     const int T = 2 * s + (g >> 1), gp = 2 * (g & 1) + jh;
 #if NR_BF1
     store_slot(f32x4{v[0], v[1], v[2], v[3]}, blk, (T * 2 + S) * 64 + 16 * gp + (lane & 15));
 #else
-    *reinterpret_cast<f32x4*>(blk + ((T * 2 + S) * 64 + 16 * gp + (lane & 15)) * 4) =
+    *reinterpret_cast<f32x4*>(blk + (16 * S + (lane & 15)) * W + 16 * T + 4 * gp) =
         f32x4{v[0], v[1], v[2], v[3]};
 #endif
 }
@@ -156,7 +158,7 @@ struct PeSide {
         if constexpr (SAVE) {
             if (t == 2 || t == 6) {
                 const int u = 2 * GC::value + (t == 6), S = u >> 2, s = (u >> 1) & 1, jh = u & 1;
-                store_pe4(&pe[S][8 * s + 4 * jh], s, jh, S, g, dst, lane);
+                store_pe4<64>(&pe[S][8 * s + 4 * jh], s, jh, S, g, dst, lane);
             }
         }
     }
@@ -174,7 +176,7 @@ struct DirPeSide {
         if constexpr (SAVE) {
             if (t & 1) {
                 const int u = t >> 1;
-                store_pe4(&dpe[u >> 1][4 * (u & 1)], 0, u & 1, u >> 1, g, dst, lane);
+                store_pe4<32>(&dpe[u >> 1][4 * (u & 1)], 0, u & 1, u >> 1, g, dst, lane);
             }
         }
     }
@@ -224,7 +226,7 @@ struct AccU {
             } else {
                 const int F = 2 * s + (p >> 1);
                 const f32x4 v = {pend[0], pend[1], x0, x1};
-                store_n16(v, F, sb, dst, lane);
+                store_row<256>(v, F, sb, dst, lane);
                 if constexpr (MASK) {
                     mask_bits(v, F, sb, w);
                     if (s == 7 && sb == 1 && p == 3)
@@ -515,7 +517,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
                     f32x4 v = C[F][S];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] = relu_i(v[r]) * kWUnscale;
-                    store_n16(v, F, S, hd, lane);
+                    store_row<128>(v, F, S, hd, lane);
                     mask_bits(v, F, S, w);
                 }
             *reinterpret_cast<uint4*>(mseg(8) + lane * 4) = make_uint4(w[0], w[1], w[2], w[3]);

@@ -373,9 +373,12 @@ struct Geo3 {
     }
 };
 
-// one operand's half-block: loads (2 float4 per thread) and the split/store
-template <int KIND, int W>
+// one operand's half-block: loads (2 float4 per thread) and the split/store.
+// ROWS: an input segment saved sample-major (x3.h store_row: row width
+// RW = the segment's columns); else N16 slots (gradient segments)
+template <int KIND, int W, bool ROWS = false>
 struct Stager {
+    static constexpr int RW = Geo3<KIND, W>::CHUNKS * 8;
     bool act;      // this thread owns a pair (loads run for every thread, clamped)
     int k, h, jp;  // chunk, lane half, sample pair
     f32x4 v0, v1;
@@ -402,9 +405,15 @@ struct Stager {
                                  x3::bf16_slot(Geo3<KIND, W>::f4(k, h, hb, 2 * jp));
             v0 = x3::unpack_bf16x4(p[0]); v1 = x3::unpack_bf16x4(p[4]);
 #else
-            const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * F4 +
-                             Geo3<KIND, W>::f4(k, h, hb, 2 * jp);
-            v0 = ld_seg(p); v1 = ld_seg(p + 1);
+            if constexpr (ROWS) {
+                const float* r = base + ((size_t)blk * 32 + 16 * hb + 2 * jp) * RW + Geo3<KIND, W>::col(k, h);
+                v0 = ld_seg(reinterpret_cast<const f32x4*>(r));
+                v1 = ld_seg(reinterpret_cast<const f32x4*>(r + RW));
+            } else {
+                const f32x4* p = reinterpret_cast<const f32x4*>(base) + (size_t)blk * F4 +
+                                 Geo3<KIND, W>::f4(k, h, hb, 2 * jp);
+                v0 = ld_seg(p); v1 = ld_seg(p + 1);
+            }
 #endif
         }
     }
@@ -415,10 +424,9 @@ struct Stager {
 #if NR_BF1
         (void)base; (void)s0; (void)s1;
 #else
-        constexpr int F4 = Geo3<KIND, W>::CHUNKS * 64;
-        const f32x4* b = reinterpret_cast<const f32x4*>(base);
-        v0 = ld_seg(b + (size_t)(s0 >> 5) * F4 + Geo3<KIND, W>::f4(k, h, (s0 >> 4) & 1, s0 & 15));
-        v1 = ld_seg(b + (size_t)(s1 >> 5) * F4 + Geo3<KIND, W>::f4(k, h, (s1 >> 4) & 1, s1 & 15));
+        static_assert(ROWS, "gathered operands are input segments (sample-major rows)");
+        v0 = ld_seg(reinterpret_cast<const f32x4*>(base + (size_t)s0 * RW + Geo3<KIND, W>::col(k, h)));
+        v1 = ld_seg(reinterpret_cast<const f32x4*>(base + (size_t)s1 * RW + Geo3<KIND, W>::col(k, h)));
 #endif
     }
     // split + store column e of this thread's chunk into an operand image
@@ -442,7 +450,8 @@ struct Stager {
 // A fused task's extra operand, staged thin: thread q < W * 8 loads one float2
 // (columns 2cp, 2cp + 1 of sample j of the half-block, q = 16 cp + j) -- 2
 // registers per set instead of Stager's 8 -- and writes single pieces.
-template <int KIND, int W>
+// ROWS: an input segment (sample-major rows of W), else the head gradient.
+template <int KIND, int W, bool ROWS = false>
 struct ThinStager {
     static constexpr int Q = W * 8;            // float2 per half-block
     bool act;
@@ -456,6 +465,7 @@ struct ThinStager {
     __device__ __forceinline__ void load(const float* base, int blk, int hb) {
         size_t f;   // float offset of the pair
         if constexpr (KIND == SEG_HEAD) f = 4 * ((size_t)blk * 32 + 16 * hb + j) + c;
+        else if constexpr (ROWS) f = ((size_t)blk * 32 + 16 * hb + j) * W + c;
         else f = 4 * ((size_t)blk * (W / 8) * 64 + ((c >> 4) * 2 + hb) * 64 + 16 * ((c & 15) >> 2) + j) + (c & 3);
 #if NR_BF1
         static_assert(KIND == SEG_HEAD, "bf16 runs no fused task pairs (kFuse)");
@@ -464,9 +474,8 @@ struct ThinStager {
     }
     // the same pair of sample s (gathered, see Stager::load_g)
     __device__ __forceinline__ void load_g(const float* base, int s) {
-        const size_t f = 4 * ((size_t)(s >> 5) * (W / 8) * 64 + ((c >> 4) * 2 + ((s >> 4) & 1)) * 64 +
-                              16 * ((c & 15) >> 2) + (s & 15)) + (c & 3);
-        v = ld_seg(reinterpret_cast<const x3::f32x2*>(base + f));
+        static_assert(ROWS, "gathered operands are input segments (sample-major rows)");
+        v = ld_seg(reinterpret_cast<const x3::f32x2*>(base + (size_t)s * W + c));
     }
     // split + store this thread's pair (times sc); s0/s1 += the unscaled values
     __device__ __forceinline__ void store(char* img, int nval, float& s0, float& s1, float sc) {
@@ -544,9 +553,9 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
     float xbacc[2] = {0.f, 0.f};
 
     // two register sets per operand: the loads run two stages ahead
-    Stager<KA, WA> sa[2];
-    Stager<KB, WB> sb[2];
-    ThinStager<XKK, XWW> sx[2];
+    Stager<KA, WA> sa[2];          // gradient operand (N16 slots, by position)
+    Stager<KB, WB, true> sb[2];    // input operand (sample-major rows)
+    ThinStager<XKK, XWW, HX && XS == 0> sx[2];
     sa[0].init(tid); sa[1].init(tid);
     sb[0].init(tid); sb[1].init(tid);
     if constexpr (HX) { sx[0].init(tid); sx[1].init(tid); }

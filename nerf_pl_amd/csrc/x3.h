@@ -633,7 +633,7 @@ __device__ __forceinline__ void store_slot(const f32x4& v, float* __restrict__ s
     f32x4* p = reinterpret_cast<f32x4*>(seg) + idx;
 #if NR_X3_DBG == 9
     asm volatile("" ::"v"(v), "v"(p));
-#elif NR_NT_STORE
+#elif NR_NT_STORE && NR_ROW_NT
     __builtin_nontemporal_store(v, p);
 #else
     *p = v;
@@ -653,6 +653,33 @@ __device__ __forceinline__ void store_n16(const f32x4& v, int F, int S, float* _
     __builtin_nontemporal_store(v, p);     // streamed: keep L2 for the weight ring
 #else
     *p = v;
+#endif
+}
+
+// A forward activation saved for the weight gradient (f16x3 / bf16x6):
+// sample-major rows of W floats, block of 32 samples after block -- the
+// lane's four values (features 16 F + 4 g .. +3 of sample 16 S + j, lane =
+// 16 g + j) go to row 16 S + j.  A store instruction writes 16 rows x 64 B;
+// the weight gradient then reads any sample's row contiguously, so gathering
+// the samples with a nonzero output gradient (active.hip) moves only their
+// bytes.  The bf16 variant keeps its N16 slots (store_slot, read by LDS-DMA).
+#ifndef NR_ROW_NT
+#define NR_ROW_NT 1      // row stores non-temporal like the N16 ones (A/B knob)
+#endif
+template <int W>
+__device__ __forceinline__ void store_row(const f32x4& v, int F, int S, float* __restrict__ blk,
+                                          int lane) {
+#if NR_BF1
+    store_n16(v, F, S, blk, lane);
+#else
+    f32x4* p = reinterpret_cast<f32x4*>(blk + (16 * S + (lane & 15)) * W + 16 * F + 4 * (lane >> 4));
+#if NR_X3_DBG == 9
+    asm volatile("" ::"v"(v), "v"(p));
+#elif NR_NT_STORE && NR_ROW_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
 #endif
 }
 

@@ -298,6 +298,14 @@ def n16_to_rows(seg: torch.Tensor, n: int, width: int) -> torch.Tensor:
     return x.permute(0, 2, 4, 1, 3, 5).reshape(nb * BLK, width)[:n]
 
 
+def saved_rows(seg: torch.Tensor, n: int, width: int) -> torch.Tensor:
+    """An activation segment of the split arithmetics' training forward
+    (csrc/x3.h store_row): sample-major rows of ``width`` values (PE segments:
+    columns are PE slots, packing.PE16_MAP / DIR16_MAP) -> (n, width)."""
+    nb = n_blocks(n)
+    return seg[: nb * BLK * width].view(nb * BLK, width)[:n]
+
+
 def pe_to_rows(seg: torch.Tensor, n: int, ksteps: int) -> torch.Tensor:
     """Decode a PE segment [block][g/4][lane][g%4] to (n, 2*ksteps) rows with
     column 32h+g (xyz, ksteps=32) / 16h+g (dir, ksteps=16) = pe value (g, h)."""

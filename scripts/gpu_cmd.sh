@@ -1,12 +1,11 @@
-# scratch GPU command (gpurun): full check of the tree + profiles of the
-# zero-gradient-sample backward
+# scratch GPU command (gpurun): same-box A/B of the saved-activation layouts
 set -o pipefail
-mkdir -p gpurun_out/pmcb
-B="python bench.py --steps 3 --warmup 2 --cpu-baseline-seconds 0 --fp32-leg-steps 0 --no-kernel-timing"
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/tests.log 2>&1 || exit $?
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py --config cfg5 --grad-on-light --steps 10 --warmup 3 --cpu-baseline-seconds 0 > gpurun_out/bench_cfg5gol.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-baseline-seconds 0 --no-kernel-timing > gpurun_out/prof.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmcb/fetch -o run --output-format csv -- $B > gpurun_out/pmcb/fetch.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmcb/write -o run --output-format csv -- $B > gpurun_out/pmcb/write.log 2>&1
+mkdir -p gpurun_out/ab
+B="python bench.py --steps 10 --warmup 3 --cpu-baseline-seconds 0 --fp32-leg-steps 0"
+for r in 1 2; do
+for v in n16 rows rowplain; do
+  case $v in n16) L=dev/ab/libnerf_pl_amd_n16.so ;; rows) L=nerf_pl_amd/libnerf_pl_amd.so ;; rowplain) L=dev/ab/libnerf_pl_amd_rowplain.so ;; esac
+  NERF_PL_AMD_LIB=$L timeout -k 10 200 $B > gpurun_out/ab/cfg2_${v}_$r.log 2>&1 || exit $?
+  if [ $r = 1 ]; then NERF_PL_AMD_LIB=$L timeout -k 10 200 $B --config cfg5 --grad-on-light > gpurun_out/ab/cfg5gol_${v}.log 2>&1 || exit $?; fi
+done
+done

@@ -228,20 +228,21 @@ def test_mlp_forward_saved_activations(math):
 
 
 def _check_saved_n16(seg, n, e_xyz, e_dir, hs, feat, hdir):
-    """bf16x6 pipeline: every segment in x3.h's N16 layout, PE by slot."""
+    """split arithmetics: every activation segment in sample-major rows
+    (x3.h store_row), PE by slot; the ReLU masks in lane words."""
     from nerf_pl_amd import ops, packing
     for name, emb, smap in (("pe", e_xyz, packing.PE16_MAP), ("dirpe", e_dir, packing.DIR16_MAP)):
-        pe = ops.n16_to_rows(seg[name], n, len(smap))
+        pe = ops.saved_rows(seg[name], n, len(smap))
         for q, f in enumerate(smap):
             if f < 0:
                 assert torch.all(pe[:, q] == 0), (name, q)
             else:
                 torch.testing.assert_close(pe[:, q], emb[:, f], rtol=0, atol=2e-6)
     for l in range(8):
-        got = ops.n16_to_rows(seg[f"h{l+1}"], n, 256)
+        got = ops.saved_rows(seg[f"h{l+1}"], n, 256)
         assert (got - hs[l]).abs().max().item() < 2e-5, f"h{l+1}"
-    assert (ops.n16_to_rows(seg["feat"], n, 256) - feat).abs().max().item() < 2e-5
-    assert (ops.n16_to_rows(seg["hdir"], n, 128) - hdir).abs().max().item() < 2e-5
+    assert (ops.saved_rows(seg["feat"], n, 256) - feat).abs().max().item() < 2e-5
+    assert (ops.saved_rows(seg["hdir"], n, 128) - hdir).abs().max().item() < 2e-5
     # ReLU bit masks: lane 16g+j, word F>>2, bit 8(F&3)+4S+r <-> feature 16F+4g+r
     # of sample 32b+16S+j is > 0
     nb = ops.n_blocks(n)
