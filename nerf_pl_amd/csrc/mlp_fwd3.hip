@@ -129,16 +129,21 @@ __device__ __forceinline__ void dir_gather(float (&d)[8], const float* __restric
 
 // slot values 4u .. 4u+3 (u = 2s + jh of the lane's 8-slot cells) -> the
 // saved slots 32s + 8g + 4jh = tile 2s + (g >> 1), group 2(g & 1) + jh: N16
-// (bf16) or the sample-major rows of W slots (x3.h store_row)
-template <int W>
+// (bf16, and the sigma-only training forward) or the sample-major rows of W
+// slots (ROWS, x3.h store_row)
+template <int W, bool ROWS>
 __device__ __forceinline__ void store_pe4(const float* v, int s, int jh, int S, int g,
                                           float* __restrict__ blk, int lane) {
     const int T = 2 * s + (g >> 1), gp = 2 * (g & 1) + jh;
 #if NR_BF1
     store_slot(f32x4{v[0], v[1], v[2], v[3]}, blk, (T * 2 + S) * 64 + 16 * gp + (lane & 15));
 #else
-    *reinterpret_cast<f32x4*>(blk + (16 * S + (lane & 15)) * W + 16 * T + 4 * gp) =
-        f32x4{v[0], v[1], v[2], v[3]};
+    if constexpr (ROWS)
+        *reinterpret_cast<f32x4*>(blk + (16 * S + (lane & 15)) * W + 16 * T + 4 * gp) =
+            f32x4{v[0], v[1], v[2], v[3]};
+    else
+        *reinterpret_cast<f32x4*>(blk + ((T * 2 + S) * 64 + 16 * gp + (lane & 15)) * 4) =
+            f32x4{v[0], v[1], v[2], v[3]};
 #endif
 }
 
@@ -146,8 +151,8 @@ struct MaskWords { uint32_t w[4] = {0u, 0u, 0u, 0u}; };
 
 enum FwdMode { FWD_RAYS = 0, FWD_EMB = 1, FWD_PTS = 2 };
 
-// layer 1's side: the xyz PE slots saved N16, 2 float4 per group (tiles 2, 6)
-template <bool SAVE>
+// layer 1's side: the xyz PE slots saved, 2 float4 per group (tiles 2, 6)
+template <bool SAVE, bool ROWS>
 struct PeSide {
     static constexpr int kBefore7 = SAVE ? 2 : 0;
     const float (&pe)[2][16];
@@ -158,7 +163,7 @@ struct PeSide {
         if constexpr (SAVE) {
             if (t == 2 || t == 6) {
                 const int u = 2 * GC::value + (t == 6), S = u >> 2, s = (u >> 1) & 1, jh = u & 1;
-                store_pe4<64>(&pe[S][8 * s + 4 * jh], s, jh, S, g, dst, lane);
+                store_pe4<64, ROWS>(&pe[S][8 * s + 4 * jh], s, jh, S, g, dst, lane);
             }
         }
     }
@@ -176,7 +181,7 @@ struct DirPeSide {
         if constexpr (SAVE) {
             if (t & 1) {
                 const int u = t >> 1;
-                store_pe4<32>(&dpe[u >> 1][4 * (u & 1)], 0, u & 1, u >> 1, g, dst, lane);
+                store_pe4<32, true>(&dpe[u >> 1][4 * (u & 1)], 0, u & 1, u >> 1, g, dst, lane);
             }
         }
     }
@@ -194,7 +199,9 @@ struct Fwd3Args {
 // units p = 0, 1 of (k-step s, tile S) complete feature tile 2s, p = 2, 3 tile
 // 2s+1 -- with their ReLU bits (MASK); SIG accumulates the sigma head
 // w_sigma . x over the split values (x = h8), so no pass re-reads h8.
-template <bool RELU, bool STORE, bool MASK, bool SIG>
+// ROWS: saved as sample-major rows (the full graph, x3.h store_row), else N16
+// (the sigma-only training forward, whose backward gathers almost nothing)
+template <bool RELU, bool STORE, bool MASK, bool SIG, bool ROWS = true>
 struct AccU {
     static constexpr bool kStores = STORE;
     template <typename P> __device__ __forceinline__ void begin(const P&) {}
@@ -226,7 +233,8 @@ struct AccU {
             } else {
                 const int F = 2 * s + (p >> 1);
                 const f32x4 v = {pend[0], pend[1], x0, x1};
-                store_row<256>(v, F, sb, dst, lane);
+                if constexpr (ROWS) store_row<256>(v, F, sb, dst, lane);
+                else store_n16(v, F, sb, dst, lane);
                 if constexpr (MASK) {
                     mask_bits(v, F, sb, w);
                     if (s == 7 && sb == 1 && p == 3)
@@ -378,14 +386,17 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     NoNext nonext;
     ZeroInit zero;
     auto bias = [&](int off) { return BiasInit{H + off, g}; };
-    using U = AccU<true, SAVE, SAVE, false>;
+    // the full graph saves sample-major rows, the sigma-only training forward N16
+    // (wgrad.hip reads each as its task list expects)
+    constexpr bool kRows = !SIGMA_ONLY;
+    using U = AccU<true, SAVE, SAVE, false, kRows>;
 
     // layer 1: PE(63) -> 256; stores the PE slots
     PeU<16> peu{pe};
     split_all(peu, b);
     U u1{A, hseg(0), mseg(0), nullptr, lane, g};
     {
-        PeSide<SAVE> side{pe, SV + (size_t)blk * NR_SEGF(64), g, lane};
+        PeSide<SAVE, kRows> side{pe, SV + (size_t)blk * NR_SEGF(64), g, lane};
         auto bi = bias(NR_H_BIAS(1));
         segment<FwdTab, kL1, 2, 2, QEND, true>(dma, lane, A, peu, u1, bi, side, b, f0);
     }
@@ -431,7 +442,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         // splitting h8 for xyz_encoding_final, and sigma comes from the same
         // sums; out rows are (n, 4) [0, 0, 0, sigma] for the backward's contract
         { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, nonext, bi, none, b, f0); }
-        AccU<true, true, true, true> u8{B, hseg(7), mseg(7), H + NR_H_WSIG, lane, g};
+        AccU<true, true, true, true, false> u8{B, hseg(7), mseg(7), H + NR_H_WSIG, lane, g};
         drain_all(u8);
         float sigma[2];
 #pragma unroll

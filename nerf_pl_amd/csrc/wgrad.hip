@@ -424,9 +424,15 @@ struct Stager {
 #if NR_BF1
         (void)base; (void)s0; (void)s1;
 #else
-        static_assert(ROWS, "gathered operands are input segments (sample-major rows)");
-        v0 = ld_seg(reinterpret_cast<const f32x4*>(base + (size_t)s0 * RW + Geo3<KIND, W>::col(k, h)));
-        v1 = ld_seg(reinterpret_cast<const f32x4*>(base + (size_t)s1 * RW + Geo3<KIND, W>::col(k, h)));
+        if constexpr (ROWS) {
+            v0 = ld_seg(reinterpret_cast<const f32x4*>(base + (size_t)s0 * RW + Geo3<KIND, W>::col(k, h)));
+            v1 = ld_seg(reinterpret_cast<const f32x4*>(base + (size_t)s1 * RW + Geo3<KIND, W>::col(k, h)));
+        } else {    // N16: block s / 32, half-block (s / 16) & 1, lane column s & 15
+            constexpr int F4 = Geo3<KIND, W>::CHUNKS * 64;
+            const f32x4* b = reinterpret_cast<const f32x4*>(base);
+            v0 = ld_seg(b + (size_t)(s0 >> 5) * F4 + Geo3<KIND, W>::f4(k, h, (s0 >> 4) & 1, s0 & 15));
+            v1 = ld_seg(b + (size_t)(s1 >> 5) * F4 + Geo3<KIND, W>::f4(k, h, (s1 >> 4) & 1, s1 & 15));
+        }
 #endif
     }
     // split + store column e of this thread's chunk into an operand image
@@ -474,8 +480,11 @@ struct ThinStager {
     }
     // the same pair of sample s (gathered, see Stager::load_g)
     __device__ __forceinline__ void load_g(const float* base, int s) {
-        static_assert(ROWS, "gathered operands are input segments (sample-major rows)");
-        v = ld_seg(reinterpret_cast<const x3::f32x2*>(base + (size_t)s * W + c));
+        static_assert(KIND != SEG_HEAD, "head segments are gradients (packed by position)");
+        const size_t f = ROWS ? (size_t)s * W + c
+                              : 4 * ((size_t)(s >> 5) * (W / 8) * 64 + ((c >> 4) * 2 + ((s >> 4) & 1)) * 64 +
+                                     16 * ((c & 15) >> 2) + (s & 15)) + (c & 3);
+        v = ld_seg(reinterpret_cast<const x3::f32x2*>(base + f));
     }
     // split + store this thread's pair (times sc); s0/s1 += the unscaled values
     __device__ __forceinline__ void store(char* img, int nval, float& s0, float& s1, float sc) {
@@ -515,8 +524,8 @@ __device__ __forceinline__ x3::Pieces frag(const char* q, int plane) {
 // 4-row head: extra output XW x N); its XWM x XWN wave grid covers the extra
 // output (grids smaller than 8 waves are computed twice, written once) and the
 // result goes to the partner task's slab `xslab`.
-template <bool GA, int KA, int WA, int KB, int WB, int WM, int WN, int XK = -1, int XW = 0,
-          int XS = 0, int XWM = 1, int XWN = 1>
+template <bool GA, bool ROWS, int KA, int WA, int KB, int WB, int WM, int WN, int XK = -1,
+          int XW = 0, int XS = 0, int XWM = 1, int XWN = 1>
 __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, int b0, int b1,
                                             char* lds, float* __restrict__ slab,
                                             float* __restrict__ xslab = nullptr) {
@@ -554,8 +563,8 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
 
     // two register sets per operand: the loads run two stages ahead
     Stager<KA, WA> sa[2];          // gradient operand (N16 slots, by position)
-    Stager<KB, WB, true> sb[2];    // input operand (sample-major rows)
-    ThinStager<XKK, XWW, HX && XS == 0> sx[2];
+    Stager<KB, WB, ROWS> sb[2];    // input operand (sample-major rows, or N16)
+    ThinStager<XKK, XWW, ROWS && HX && XS == 0> sx[2];
     sa[0].init(tid); sa[1].init(tid);
     sb[0].init(tid); sb[1].init(tid);
     if constexpr (HX) { sx[0].init(tid); sx[1].init(tid); }
@@ -1057,8 +1066,10 @@ __device__ __forceinline__ void wgrad_b1_body(const WgArgs& a, const WgTask& T, 
 }
 #endif  // NR_BF1
 
-// GA: the packed sample list a.slist (the *_active entry points)
-template <bool GA>
+// GA: the packed sample list a.slist (the *_active entry points); ROWS: the
+// input segments are sample-major rows (the full graph's forward), else N16
+// (the sigma-only training forward, mlp_fwd3.hip kRows)
+template <bool GA, bool ROWS>
 __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
 #if NR_BF1
     __shared__ __attribute__((aligned(16))) char lds[b1::kLds > w3::kLds ? b1::kLds : w3::kLds];
@@ -1093,17 +1104,17 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
         switch (__builtin_amdgcn_readfirstlane(T.id)) {
 #if NR_WGRAD_FUSE_MASK & 1
             case 5:    // DZ(4) x [H(3) | PE]: xyz_encoding_5 (skip layer)
-                wgrad3_body<GA, SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_PE, 64, 0, NR_WG_PE_WM, 8 / NR_WG_PE_WM>(
+                wgrad3_body<GA, ROWS, SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_PE, 64, 0, NR_WG_PE_WM, 8 / NR_WG_PE_WM>(
                     a, T, b0, b1, lds, slab, xslab); break;
 #endif
 #if NR_WGRAD_FUSE_MASK & 2
             case 9:    // [DZ(8) | head] x H(7): xyz_encoding_final and sigma
-                wgrad3_body<GA, SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_HEAD, 4, 1, 1, 8>(
+                wgrad3_body<GA, ROWS, SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_HEAD, 4, 1, 1, 8>(
                     a, T, b0, b1, lds, slab, xslab); break;
 #endif
 #if NR_WGRAD_FUSE_MASK & 4
             case 10:   // dz_dir x [feat | dir PE]: dir_encoding
-                wgrad3_body<GA, SEG_ACC, 128, SEG_ACC, 256, 2, 4, SEG_DPE, 32, 0, 4, 1>(
+                wgrad3_body<GA, ROWS, SEG_ACC, 128, SEG_ACC, 256, 2, 4, SEG_DPE, 32, 0, 4, 1>(
                     a, T, b0, b1, lds, slab, xslab); break;
 #endif
         }
@@ -1128,17 +1139,17 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
 #endif
     switch (__builtin_amdgcn_readfirstlane(T.id)) {
         case 0: case 4:
-            wgrad3_body<GA, SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, ROWS, SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
         case 10:
-            wgrad3_body<GA, SEG_ACC, 128, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, ROWS, SEG_ACC, 128, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
         case 11:
-            wgrad3_body<GA, SEG_ACC, 128, SEG_DPE, 32, 4, 1>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, ROWS, SEG_ACC, 128, SEG_DPE, 32, 4, 1>(a, T, b0, b1, lds, slab); break;
         case 12:
-            wgrad3_body<GA, SEG_HEAD, 4, SEG_ACC, 256, 1, 8>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, ROWS, SEG_HEAD, 4, SEG_ACC, 256, 1, 8>(a, T, b0, b1, lds, slab); break;
         case 13:
-            wgrad3_body<GA, SEG_HEAD, 4, SEG_ACC, 128, 1, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, ROWS, SEG_HEAD, 4, SEG_ACC, 128, 1, 4>(a, T, b0, b1, lds, slab); break;
         default:
-            wgrad3_body<GA, SEG_ACC, 256, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad3_body<GA, ROWS, SEG_ACC, 256, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
     }
 }
 
@@ -1374,13 +1385,17 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
 #if NR_F16
     stats_reduce_kernel<<<NR_STAT_SEGS, kStatT, 0, st>>>(SV + nr_sv_stats(nbp), (int)nbp);
     NR_LAUNCH_CHECK("nr_wgrad_stats");
-    if (slist) wgrad3_kernel<true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
-    else wgrad3_kernel<false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    if (slist && !sigma_only) wgrad3_kernel<true, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (slist) wgrad3_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (!sigma_only) wgrad3_kernel<false, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else wgrad3_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #elif NR_BF1
-    wgrad3_kernel<false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    wgrad3_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #else
-    if (x3 && slist) wgrad3_kernel<true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
-    else if (x3) wgrad3_kernel<false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    if (x3 && slist && !sigma_only) wgrad3_kernel<true, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (x3 && slist) wgrad3_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (x3 && !sigma_only) wgrad3_kernel<false, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (x3) wgrad3_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else wgrad_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #endif
     NR_LAUNCH_CHECK("nr_wgrad");
