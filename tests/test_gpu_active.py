@@ -110,7 +110,7 @@ CASES = ("dense", "scattered", "blocks", "runs", "one", "none")
 @pytest.mark.parametrize("math", ["f16x3", "bf16x6"])
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("sigma_only", [False, True])
-def test_active_backward_matches_every_block(math, case, sigma_only, monkeypatch):
+def test_active_backward_matches_every_sample(math, case, sigma_only, monkeypatch):
     fn = _zeroed(case)
     a = _mlp_grads(math, True, fn, monkeypatch, sigma_only=sigma_only)
     b = _mlp_grads(math, False, fn, monkeypatch, sigma_only=sigma_only)
@@ -127,7 +127,7 @@ def test_active_backward_matches_every_block(math, case, sigma_only, monkeypatch
 
 def test_active_backward_in_render_rays(monkeypatch):
     """the training step of render_rays (both models, coarse + fine) with and
-    without the block list: same loss, same gradients (1e-6 normwise)"""
+    without the sample list: same loss, same gradients (1e-6 normwise)"""
     from nerf_pl_amd import Embedding, NeRF, ReplayRNG, functions, ops
     from nerf_pl_amd.rays import blender_rays
     monkeypatch.setattr(ops, "MATH", "f16x3")
