@@ -8,7 +8,12 @@ all 16M pixels, like the reference's shuffled DataLoader over its ray buffer,
 with the target colours gathered in the same pass) -> render_rays (64 coarse +
 128 fine, perturb=1, noise_std=1: opt.py defaults) -> MSE(coarse)+MSE(fine) ->
 backward -> [RCCL all-reduce of the 4.77 MB gradient when N>1] -> Adam(lr=5e-4,
-eps=1e-8) as one fused launch.
+eps=1e-8) as one fused launch.  The backward of the split arithmetics runs over
+the samples whose output gradient is nonzero (nr_active_samples, DESIGN.md 10:
+the other samples add exact zeros, so the gradients are the every-sample
+backward's up to the order of the split-K sums); the line's
+``backward_samples`` reports the share listed per pass, and the rooflines of
+the backward kernels count only those samples' work.
 
 The other BASELINE.json configs are selectable (``--config``; the driver's
 default run is cfg2):
