@@ -177,10 +177,27 @@ def parse():
                     help="cfg5: Light_N_importance (default 64; -1 = a random choice of "
                          "{0, 8, 16, 32} per step, train_efficient_sm.py:153-154, drawn from a "
                          "generator seeded alike on every rank)")
-    ap.add_argument("--fp32-leg-steps", type=int, default=5,
-                    help="after the timed region, time this many steps with the exact fp32 "
-                         "MLP arithmetic (v_mfma_f32_32x32x2_f32) for the fp32-MFMA roofline; "
-                         "0 disables")
+    ap.add_argument("--fp32-leg-steps", type=int, default=None,
+                    help="after the timed region, time this many steps (after --warmup "
+                         "untimed ones) with the exact fp32 MLP arithmetic "
+                         "(v_mfma_f32_32x32x2_f32) for the fp32-MFMA roofline; default: "
+                         "--steps; 0 disables")
+    # the hot-path hyperparameters of opt.py:18-37 (same names, same meaning); None
+    # keeps the workload's own default (cfg2-4: the opt.py defaults; cfg5: the
+    # noise_std=0 of every train_efficient_sm launcher; eval: eval.py's 0/0)
+    ap.add_argument("--perturb", type=float, default=None,
+                    help="opt.py --perturb: factor to perturb depth sampling points")
+    ap.add_argument("--noise-std", type=float, default=None,
+                    help="opt.py --noise_std: std dev of the noise added to sigma")
+    ap.add_argument("--lr", type=float, default=5e-4, help="opt.py --lr (Adam)")
+    ap.add_argument("--chunk", type=int, default=32 * 1024,
+                    help="opt.py --chunk: the batch is rendered in chunks of this many rays "
+                         "(NeRFSystem.forward, train.py:49-71), one render_rays call each")
+    ap.add_argument("--use-disp", action="store_true",
+                    help="opt.py --use_disp: sample linearly in inverse depth")
+    ap.add_argument("--white-back", action="store_true",
+                    help="the dataset's white_back (blender.py:21 sets it False; "
+                         "blender_efficient_sm.py:22 True)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                     help="weak: --batch rays per rank (the driver's default); strong: --batch "
                          "rays per step in total, split over the ranks (SURVEY 8e)")
@@ -198,7 +215,33 @@ def parse():
     a.n_importance = a.n_importance if a.n_importance is not None else d[3]
     if a.light_importance is None:
         a.light_importance = a.n_importance
+    if a.fp32_leg_steps is None:
+        a.fp32_leg_steps = a.steps
+    if a.chunk <= 0:
+        ap.error("--chunk must be positive")
+    dflt = {"cfg5": (1.0, 0.0), "eval": (0.0, 0.0)}.get(a.config, (1.0, 1.0))
+    a.perturb = dflt[0] if a.perturb is None else a.perturb
+    a.noise_std = dflt[1] if a.noise_std is None else a.noise_std
     return a
+
+
+def hyper(a):
+    """the opt.py hyperparameters a workload line states"""
+    return (f"perturb={a.perturb:g}, noise_std={a.noise_std:g}"
+            + (", use_disp" if a.use_disp else "") + (", white_back" if a.white_back else "")
+            + (f", chunk={a.chunk}" if a.chunk != 32 * 1024 else ""))
+
+
+def render_chunked(render, models, emb, rays, a, S, I, test_time=False, **kw):
+    """NeRFSystem.forward (train.py:49-71): render the batch in chunks of
+    ``a.chunk`` rays, one render_rays call each, and concatenate the results."""
+    B = rays.shape[0]
+    if B <= a.chunk:
+        return render(models, emb, rays, S, a.use_disp, a.perturb, a.noise_std, I, a.chunk,
+                      a.white_back, test_time, **kw)
+    parts = [render(models, emb, rays[i:i + a.chunk], S, a.use_disp, a.perturb, a.noise_std, I,
+                    a.chunk, a.white_back, test_time, **kw) for i in range(0, B, a.chunk)]
+    return {k: torch.cat([p[k] for p in parts], 0) for k in parts[0]}
 
 
 class KernelTimer:
@@ -334,12 +377,12 @@ def cpu_train(args, budget_s, rays_all, label):
     torch.manual_seed(0)
     b = 256 if threads == 1 else args.batch
     params = [{k: v.requires_grad_(True) for k, v in O.make_params(s).items()} for s in (1, 2)]
-    opt = torch.optim.Adam([p for d in params for p in d.values()], lr=5e-4)
+    opt = torch.optim.Adam([p for d in params for p in d.values()], lr=args.lr)
 
     def step():
         idx = torch.randint(0, rays_all.shape[0], (b,))
-        res = O.render_rays(params, rays_all[idx], args.n_samples, False, 1.0, 1.0,
-                            args.n_importance, 32768, False)
+        res = render_chunked(lambda m, e, *r: O.render_rays(m, *r), params, None, rays_all[idx],
+                             args, args.n_samples, args.n_importance)
         loss = O.mse_loss(res, torch.rand(b, 3))
         opt.zero_grad()
         loss.backward()
@@ -348,7 +391,8 @@ def cpu_train(args, budget_s, rays_all, label):
     return dict(value=n * b / el, unit="rays/s", cores=threads, kind="port",
                 host=host_cpus(),
                 sample=f"{n} oracle training steps x {b} rays ({label}, {args.n_samples}+"
-                       f"{args.n_importance} samples, fwd+bwd+Adam) in {el:.1f} s, torch CPU "
+                       f"{args.n_importance} samples, perturb {args.perturb}, noise_std "
+                       f"{args.noise_std}, fwd+bwd+Adam) in {el:.1f} s, torch CPU "
                        f"{threads} threads")
 
 
@@ -363,8 +407,8 @@ def cpu_eval(args, budget_s, rays_all):
         rays = rays_all[pos[0]:pos[0] + b]
         pos[0] = (pos[0] + b) % (rays_all.shape[0] - b)
         with torch.no_grad():
-            O.render_rays(params, rays, args.n_samples, False, 0.0, 0.0, args.n_importance,
-                          32768, False, True)
+            render_chunked(lambda m, e, *r: O.render_rays(m, *r), params, None, rays, args,
+                           args.n_samples, args.n_importance, True)
     n, el = _timed_loop(step, budget_s)
     return dict(value=n * b / el, unit="rays/s", cores=threads, kind="port",
                 sample=f"{n} oracle test_time renders x {b} rays ({args.n_samples}+"
@@ -383,7 +427,7 @@ def cpu_shadow(args, budget_s, scene):
     threads = _cpu_threads()
     torch.manual_seed(0)
     params = [{k: v.requires_grad_(True) for k, v in O.make_params(s).items()} for s in (1, 2)]
-    opt = torch.optim.Adam([p for d in params for p in d.values()], lr=5e-4)
+    opt = torch.optim.Adam([p for d in params for p in d.values()], lr=args.lr)
     S, I, wh = args.n_samples, args.n_importance, args.img
     lrays = scene["light_rays"].cpu()
     lpix = scene["light_pixels"].cpu()
@@ -396,7 +440,8 @@ def cpu_shadow(args, budget_s, scene):
     def light_part():
         # --grad_on_light: the light render under autograd and its backward
         with torch.set_grad_enabled(args.grad_on_light):
-            res = SO.render_rays(params, lrays[:bl], S, False, 1.0, 0.0, LI, 32768, False)
+            res = SO.render_rays(params, lrays[:bl], S, args.use_disp, args.perturb,
+                                 args.noise_std, LI, args.chunk, args.white_back)
         if args.grad_on_light:
             opt.zero_grad()
             sum(v.sum() for k, v in res.items() if k.startswith("depth")).backward()
@@ -407,7 +452,8 @@ def cpu_shadow(args, budget_s, scene):
         rays = scene["rays_all"][sel].cpu()
         ppc = {"eye_pos": scene["eyes"][0].cpu().expand(b, 3),
                "camera": scene["mats"][0].cpu().expand(b, 3, 3)}
-        res = SO.render_rays(params, rays, S, False, 1.0, 0.0, I, 32768, False)
+        res = SO.render_rays(params, rays, S, args.use_disp, args.perturb, args.noise_std, I,
+                             args.chunk, args.white_back)
         out = SO.efficient_sm(scene["pixels"][sel].cpu(), lpix, res, light_map, ppc, leye, lcam,
                               (wh, wh), I > 0, LI > 0, "shadow_method_2")
         tgt = torch.rand(b, 3)
@@ -470,21 +516,22 @@ def wl_nerf_train(args, dev, rank, ndc):
 
     def step():
         rays, rgbs = sampler.next(args.batch)
-        res = render_rays(models, emb, rays, S, False, 1.0, 1.0, I, 32768, False)
+        res = render_chunked(render_rays, models, emb, rays, args, S, I)
         return loss_fn(res, rgbs)
 
+    hp = hyper(args)
     if ndc:
         name = "cfg3"
         metric = f"rays/sec ({S}c+{I}f) LLFF fern 504x378 NDC training step"
         work = (f"cfg3: LLFF fern 504x378 (20 forward-facing poses, focal 407), NDC rays "
                 f"(near/far 0/1), {S} coarse + {I} fine, batch {args.batch} rays/rank, "
-                "perturb=1, noise_std=1, MSE coarse+fine, Adam lr 5e-4")
+                f"{hp}, MSE coarse+fine, Adam lr {args.lr:g}")
         data = "synthetic (forward-facing NDC rays generated on device per batch, random target colours)"
     else:
         name = "cfg2" if args.img == 400 else f"cfg4" if args.img == 800 else f"blender{args.img}"
         metric = f"rays/sec ({S}c+{I}f) Blender-lego {W}^2 training step"
         work = (f"{name}: Blender lego {W}x{W}, {S} coarse + {I} fine, batch {args.batch} "
-                "rays/rank, perturb=1, noise_std=1, MSE coarse+fine, Adam lr 5e-4")
+                f"rays/rank, {hp}, MSE coarse+fine, Adam lr {args.lr:g}")
         data = (f"synthetic (Blender-lego {W}x{W}, {args.poses}-pose camera orbit, rays generated "
                 "on device per batch, random target colours, seeded default-init NeRF coarse+fine)")
 
@@ -521,8 +568,8 @@ def wl_eval(args, dev, rank):
         it[0] += 1
         with torch.no_grad():
             for i in range(0, rays.shape[0], args.batch):
-                render_rays(models, emb, rays[i:i + args.batch], S, False, 0.0, 0.0, I, 32768,
-                            False, True)
+                render_chunked(render_rays, models, emb, rays[i:i + args.batch], args, S, I,
+                               True)
         return None
 
     def cpu(budget):
@@ -532,7 +579,7 @@ def wl_eval(args, dev, rank):
     return dict(name="eval", metric=f"rays/sec ({S}c+{I}f) Blender-lego {W}^2 test-view render",
                 workload=f"eval: eval.py render of one {W}x{W} Blender-lego test view per step "
                          f"({W * W} rays, test_time=True: sigma-only coarse {S}, full fine "
-                         f"{S + I}; perturb=0, noise_std=0, chunks of {args.batch} rays)",
+                         f"{S + I}; {hyper(args)}, chunks of {args.batch} rays)",
                 data="synthetic (Blender-lego camera orbit, seeded default-init NeRF coarse+fine)",
                 step=step, train=False, models=models, rays_per_step=W * W,
                 samples_per_ray=S + I, flop_per_ray=S * FLOP_FWD_SIGMA + (S + I) * FLOP_FWD,
@@ -600,16 +647,17 @@ def wl_shadow(args, dev, rank):
         rays = generate_rays(scene["c2ws"], wh, wh, scene["focal"], 1.0, 200.0, sel)
         pose = sel // hw
         ppc = {"eye_pos": scene["eyes"][pose], "camera": scene["mats"][pose]}
-        cam = RS.render_rays(models, emb, rays, S, False, 1.0, 0.0, I, 32768, False)
+        cam = render_chunked(RS.render_rays, models, emb, rays, args, S, I)
         li = int(li_rng.choice([0, 8, 16, 32])) if LI == -1 else LI
         # --grad_on_light renders the light under autograd (:158-162), else no_grad (:164-168)
         with torch.set_grad_enabled(args.grad_on_light):
             if shard:
-                light = RS.render_rays_sharded(models, emb, scene["light_rays"], S, False, 1.0,
-                                               0.0, li, 32768, False)
+                light = RS.render_rays_sharded(models, emb, scene["light_rays"], S,
+                                               args.use_disp, args.perturb, args.noise_std, li,
+                                               args.chunk, args.white_back)
             else:
-                light = RS.render_rays(models, emb, scene["light_rays"], S, False, 1.0, 0.0, li,
-                                       32768, False, were_gradients_computed=False)
+                light = render_chunked(RS.render_rays, models, emb, scene["light_rays"], args, S,
+                                       li, were_gradients_computed=False)
         out = RS.efficient_sm(scene["pixels"][sel % hw], scene["light_pixels"], cam, light, ppc,
                               light_ppc, (wh, wh), I > 0, li > 0, "shadow_method_2")
         tgt = tgt_pool[sel]
@@ -626,13 +674,14 @@ def wl_shadow(args, dev, rank):
                 metric=f"camera rays/sec shadow-mapping step ({S}c+{I}f, {wh}^2 light image "
                        f"re-rendered per step{', --grad_on_light' if gol else ''})",
                 workload=f"cfg5: train_efficient_sm.py step at {wh}x{wh}: sigma-only render of "
-                         f"{B} camera rays/rank ({S}+{I}, noise_std=0, with gradients) + "
+                         f"{B} camera rays/rank ({S}+{I}, {hyper(args)}, with gradients) + "
                          f"{'autograd' if gol else 'no_grad'} render of the {hw}-ray light image "
                          f"({S}+{lname}"
                          f"{', sharded over the ranks + all-gather' if args.light_shard else ''}) + efficient_sm "
                          "(shadow_method_2, per-pose runs) + MSE + backward"
                          " + the logged OpactiyLoss"
-                         f"{' (through the light render too)' if gol else ''} + Adam lr 5e-4",
+                         f"{' (through the light render too)' if gol else ''} + Adam lr "
+                         f"{args.lr:g}",
                 data=f"synthetic ({args.poses}-pose camera orbit + one light camera, rays "
                      "generated on device, random targets, seeded default-init NeRF pair)",
                 step=step, train=True, models=models, rays_per_step=B,
@@ -655,12 +704,24 @@ def main():
     # gradient all-reduce, barriers, max-over-ranks timing) at one rank too --
     # a real-RCCL rehearsal of the driver's N-GPU run on a one-GPU box
     use_dist = world > 1 or os.environ.get("NR_BENCH_FORCE_DIST") == "1"
+    t_start = time.perf_counter()
+
+    def progress(msg):
+        """one short line per phase on stderr from every rank of a distributed
+        run (the JSON line stays rank 0's only stdout): a multi-rank run is
+        never silent for long, and a hang names its phase and rank"""
+        if use_dist:
+            print(f"[bench rank {rank}/{world} +{time.perf_counter() - t_start:.1f}s] {msg}",
+                  file=sys.stderr, flush=True)
+
     if use_dist:
         torch.cuda.set_device(local)
+        progress(f"init_process_group({backend})")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        progress("process group up")
     if args.scaling == "strong":
         if args.batch % world:
             raise SystemExit(f"--scaling strong: batch {args.batch} not divisible by {world} ranks")
@@ -686,7 +747,7 @@ def main():
     opt, reducer = None, None
     if wl["train"]:
         params = [p for m in wl["models"] for p in m.parameters()]
-        opt = FusedAdam(params, lr=5e-4, eps=1e-8)
+        opt = FusedAdam(params, lr=args.lr, eps=1e-8)
         if use_dist:
             from nerf_pl_amd.distributed import GradAllReducer
             # one bucket per model: the fine model's all-reduce overlaps the
@@ -695,6 +756,7 @@ def main():
             # first collective on the main thread: the communicator is set up
             # here, not inside the first gradient hook (autograd's thread)
             dist.barrier()
+            progress("first collective done")
 
     def step():
         loss = wl["step"]()
@@ -706,15 +768,19 @@ def main():
             opt.step()
         return loss
 
-    def run(steps, warmup):
+    def run(steps, warmup, what="main"):
         """warmup untimed steps, then `steps` timed ones between barriers;
         (seconds = max over ranks, last loss)."""
         loss = None
-        for _ in range(warmup):
+        for i in range(warmup):
             step()
+            if i == 0:
+                torch.cuda.synchronize()
+                progress(f"{what}: first warmup step done")
         if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
+        progress(f"{what}: {warmup} warmup steps done, timing {steps}")
         timer.events = {}
         if F_ is not None:
             F_.ACTIVE_LOG = []
@@ -731,6 +797,7 @@ def main():
             t = torch.tensor([el], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = t.item()
+        progress(f"{what}: timed region done ({el / max(steps, 1) * 1e3:.2f} ms/step)")
         return el, loss
 
     def rooflines(math_, ms, steps):
@@ -793,13 +860,13 @@ def main():
         from nerf_pl_amd import ops as _ops
         _ops.MATH = "fp32"
         try:
-            el32, _ = run(args.fp32_leg_steps, 2)
+            el32, _ = run(args.fp32_leg_steps, args.warmup, "fp32 leg")
         finally:
             _ops.MATH = math_main
         ms32 = el32 / args.fp32_leg_steps * 1e3
         ks32, roof32, roofs32, stage32 = rooflines("fp32", ms32, args.fp32_leg_steps)
         fp32_leg = dict(dtype="fp32", mlp_arithmetic="fp32 (v_mfma_f32_32x32x2_f32: exact fp32 "
-                        "products, fp32 accumulation)", steps=args.fp32_leg_steps, warmup=2,
+                        "products, fp32 accumulation)", steps=args.fp32_leg_steps, warmup=args.warmup,
                         value=round(wl["rays_per_step"] * world * args.fp32_leg_steps / el32, 1),
                         unit="rays/s", ms_per_step=round(ms32, 3), roofline=roof32,
                         rooflines=roofs32, mlp_stage=stage32,
@@ -808,6 +875,7 @@ def main():
 
     cpu = None
     cpu1 = None
+    progress("done")
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
         cpu = wl["cpu"](args.cpu_baseline_seconds)
         # "... and a 1-thread row too" (a third of the budget)

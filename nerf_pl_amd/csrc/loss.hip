@@ -100,7 +100,8 @@ NR_API int nr_mse_loss_bwd(const float* a, const float* b, const float* target, 
 // ---------------------------------------------------------------------------
 // losses.py:28-73 OpactiyLoss (loss_dict['opacity'], constructed by
 // train_efficient_sm.py:43 and evaluated on the light render at :191):
-//   gray = (t[:,0] + t[:,1] + t[:,2]) / 3;  sm = gray > thres, non = !sm
+//   gray = (t[:,0] + t[:,1] + t[:,2]) / 3;  sm = gray > thres, non = gray <= thres
+//   (torch.where on each comparison: a NaN grey value is in neither set)
 //   loss = coeff - |mean(o_c[non]) - mean(o_c[sm])|  [+ the same on o_f]
 // (L1Loss of two scalars), 0 when either set is empty.  The targets index the
 // opacity rows (the reference indexes the light render's opacities with the
@@ -111,9 +112,10 @@ NR_API int nr_mse_loss_bwd(const float* a, const float* b, const float* target, 
 // ---------------------------------------------------------------------------
 namespace {
 
-__device__ __forceinline__ bool op_is_sm(const float* t, int64_t i, float thres) {
+// 0: shadow pixel (gray > thres), 1: non-shadow (gray <= thres), -1: neither (NaN)
+__device__ __forceinline__ int op_set(const float* t, int64_t i, float thres) {
     const float gray = nr_add(nr_add(t[3 * i], t[3 * i + 1]), t[3 * i + 2]) / 3.0f;
-    return gray > thres;
+    return gray > thres ? 0 : (gray <= thres ? 1 : -1);
 }
 
 __global__ void __launch_bounds__(kT) opacity_fwd_kernel(const float* __restrict__ oc,
@@ -124,7 +126,8 @@ __global__ void __launch_bounds__(kT) opacity_fwd_kernel(const float* __restrict
                                                          float* __restrict__ stats) {
     double v[6] = {0, 0, 0, 0, 0, 0};   // n_sm, n_non, sum_sm_c, sum_non_c, sum_sm_f, sum_non_f
     for (int64_t i = threadIdx.x; i < n; i += kT) {
-        const int s = op_is_sm(t, i, thres) ? 0 : 1;
+        const int s = op_set(t, i, thres);
+        if (s < 0) continue;
         v[s] += 1.0;
         v[2 + s] += (double)oc[i];
         if (of) v[4 + s] += (double)of[i];
@@ -176,8 +179,9 @@ __global__ void __launch_bounds__(256) opacity_bwd_kernel(const float* __restric
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_o;
          i += (int64_t)gridDim.x * blockDim.x) {
         float vc = 0.f, vf = 0.f;
-        if (valid && i < n_t) {
-            const bool sm = op_is_sm(t, i, thres);
+        const int set = (valid && i < n_t) ? op_set(t, i, thres) : -1;
+        if (set >= 0) {
+            const bool sm = set == 0;
             const float cnt = sm ? stats[0] : stats[1];
             vc = nr_mul(gs, sm ? sc : -sc) / cnt;
             vf = nr_mul(gs, sm ? sf : -sf) / cnt;

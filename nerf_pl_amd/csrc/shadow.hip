@@ -31,6 +31,8 @@
 // rounded once (the reference uses LAPACK/BLAS in fp32 there).
 #include "common.h"
 
+#include <mutex>
+
 namespace {
 
 constexpr float kEps = 1e-5f;   // efficient_shadow_mapping.py:8
@@ -383,6 +385,37 @@ __global__ void __launch_bounds__(256) sm_normed_bwd_kernel(const float* __restr
     g_depth[i] = g[i] / nr_add(norm, kEps);
 }
 
+// The backward re-derives the workspace layout from (n, n_light) and clears
+// and atomically adds into its tail, so it must see the layout the forward
+// used.  The forward records, per workspace base address, the (n, n_light) it
+// laid out; the backward refuses any other pair (a wrong n_light would write
+// past the buffer).  Host-side and bounded: the most recent kWsSlots
+// workspaces (a training step uses one or two).
+constexpr int kWsSlots = 1024;
+struct WsRecord { const void* base; int64_t n, n_light; };
+std::mutex g_ws_mu;
+WsRecord g_ws[kWsSlots];
+int g_ws_next = 0;
+
+void ws_record(const void* base, int64_t n, int64_t n_light) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (auto& r : g_ws)
+        if (r.base == base) { r.n = n; r.n_light = n_light; return; }
+    g_ws[g_ws_next] = WsRecord{base, n, n_light};
+    g_ws_next = (g_ws_next + 1) % kWsSlots;
+}
+
+// 0: laid out by the forward for (n, n_light); 1: for another pair; 2: unknown
+int ws_check(const void* base, int64_t n, int64_t n_light, int64_t* fn, int64_t* fl) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (const auto& r : g_ws)
+        if (r.base == base) {
+            *fn = r.n; *fl = r.n_light;
+            return (r.n == n && r.n_light == n_light) ? 0 : 1;
+        }
+    return 2;
+}
+
 }  // namespace
 
 NR_API int64_t nr_sm_workspace_bytes(int64_t n, int64_t n_light) {
@@ -425,6 +458,8 @@ NR_API int nr_sm_forward(const float* pixels, const float* depth, const float* e
     if (n == 0) return 0;
     NR_REQUIRE(pixels && depth && eye && cameras && light_camera && light_eye && light_w &&
                workspace && out, "nr_sm_forward: null pointer");
+    // 64-bit fixed-point accumulators live in the tail (8-byte aligned relative to the base)
+    NR_REQUIRE(((uintptr_t)workspace & 7) == 0, "nr_sm_forward: workspace must be 8-byte aligned");
     hipStream_t st = (hipStream_t)stream;
     SmArgs a{pixels, depth, eye, cameras, per_ray, light_camera, light_eye, light_w, res_w,
              res_h, method, delta, epsilon, sigmoid, out_eps, (int)n,
@@ -437,6 +472,7 @@ NR_API int nr_sm_forward(const float* pixels, const float* depth, const float* e
         sm_norm_kernel<<<blocks, 256, 0, st>>>(a);
     }
     NR_LAUNCH_CHECK("nr_sm_forward");
+    ws_record(workspace, n, (int64_t)res_w * res_h);
     return 0;
 }
 
@@ -456,6 +492,16 @@ NR_API int nr_sm_backward(const float* g_out, void* workspace, int method, float
         return 0;
     }
     NR_REQUIRE(g_out && workspace && (g_depth || g_light_w), "nr_sm_backward: null pointer");
+    NR_REQUIRE(((uintptr_t)workspace & 7) == 0, "nr_sm_backward: workspace must be 8-byte aligned");
+    {
+        int64_t fn = 0, fl = 0;
+        const int w = ws_check(workspace, n, n_light, &fn, &fl);
+        NR_REQUIRE(w != 2, "nr_sm_backward: workspace %p was not laid out by nr_sm_forward",
+                   workspace);
+        NR_REQUIRE(w == 0, "nr_sm_backward: workspace laid out by nr_sm_forward for n=%lld rays "
+                   "and a %lld-texel light map, called with n=%lld, n_light=%lld",
+                   (long long)fn, (long long)fl, (long long)n, (long long)n_light);
+    }
     SmBwdArgs a{g_out, method, delta, epsilon, sigmoid, (int)n, (int)n_light,
                 sm_ws(workspace, n, n_light), g_depth, g_light_w};
     const unsigned blocks = (unsigned)((n + 255) / 256);

@@ -55,12 +55,15 @@ def reference_functions():
 
 
 _ALLOWED_ATTRS = {"T", "norm", "expand", "shape", "view", "stack", "reshape", "unsqueeze"}
+# torch functions get_rays / get_ndc_rays call (ray_utils.py:43, :91-92); every
+# other torch attribute (torch.load, torch.save, torch.compile, ...) is refused
+_ALLOWED_TORCH = {"stack", "norm", "ones_like", "meshgrid", "sum", "cat"}
 
 
 def _vet(defs):
     """The untrusted reference code is executed only after this check (ADVICE
     r2): plain arithmetic, subscripts and assignments over the function's own
-    names, calls only of torch.<fn> or of whitelisted tensor methods; no
+    names, calls only of whitelisted torch.<fn> or tensor methods; no
     decorators, imports, defaults that call, lambdas, comprehensions, loops,
     with-blocks, attribute access to dunders or globals other than torch."""
     ok_nodes = (ast.FunctionDef, ast.arguments, ast.arg, ast.Expr, ast.Constant, ast.Assign,
@@ -83,6 +86,7 @@ def _vet(defs):
                 assert not node.attr.startswith("_"), f"{fn.name}: dunder attribute"
                 base = node.value
                 if isinstance(base, ast.Name) and base.id == "torch":
+                    assert node.attr in _ALLOWED_TORCH, f"{fn.name}: torch.{node.attr} not allowed"
                     continue
                 assert node.attr in _ALLOWED_ATTRS, f"{fn.name}: .{node.attr} not allowed"
             if isinstance(node, ast.Name) and isinstance(node.ctx, ast.Load):

@@ -9,6 +9,7 @@ import pytest
 
 NR_EINVAL = 10001
 N = None          # null device pointer
+P = 0x10000       # a non-null (never dereferenced) device address
 
 
 def _cases():
@@ -97,6 +98,12 @@ def _cases():
         ("nr_sm_backward", [N, N, 1, 1e-3, 1e-3, 0, 4, 16, N, N, N], NR_EINVAL),  # no output
         ("nr_sm_forward", [N, N, N, N, 0, N, N, N, 128, 128, 2, 1e-3, 1e-3, 0, 1e-5, -1, N, N, N],
          NR_EINVAL),
+        # the workspace's 64-bit fixed-point accumulators need an 8-byte aligned base
+        ("nr_sm_forward", [P, P, P, P, 0, P, P, P, 8, 8, 2, 1e-3, 1e-3, 0, 1e-5, 4, P + 4, P, N],
+         NR_EINVAL),
+        ("nr_sm_backward", [P, P + 4, 2, 1e-3, 1e-3, 0, 4, 16, P, P, N], NR_EINVAL),
+        # a workspace nr_sm_forward never laid out (its n_light would be unchecked)
+        ("nr_sm_backward", [P, P + 0x1000, 2, 1e-3, 1e-3, 0, 4, 16, P, P, N], NR_EINVAL),
     ]
     return c
 

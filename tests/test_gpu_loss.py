@@ -107,15 +107,21 @@ def test_loss_checks_the_target():
         torch.testing.assert_close(u.grad, w.grad, rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize("n_t,n_o,fine,seed", [(512, 4096, True, 0), (300, 300, False, 1),
-                                               (7, 64, True, 2)])
-def test_opacity_loss_matches_reference(n_t, n_o, fine, seed):
+@pytest.mark.parametrize("n_t,n_o,fine,seed,nan", [(512, 4096, True, 0, False),
+                                                   (300, 300, False, 1, False),
+                                                   (7, 64, True, 2, False),
+                                                   (512, 1024, True, 3, True)])
+def test_opacity_loss_matches_reference(n_t, n_o, fine, seed, nan):
     """losses.py:28-73 OpactiyLoss, as train_efficient_sm.py:191 calls it: the
-    light render's opacities indexed by the camera batch's shadow pixels."""
+    light render's opacities indexed by the camera batch's shadow pixels.  A
+    target row whose grey value is NaN is in neither torch.where set (:39-40):
+    it changes neither count nor mean, and its opacity gets no gradient."""
     from oracle import nerf_oracle as O
     from nerf_pl_amd.losses import loss_dict
     g = torch.Generator().manual_seed(seed)
     tgt = torch.rand(n_t, 3, generator=g)
+    if nan:
+        tgt[::7, torch.arange(n_t)[::7] % 3] = float("nan")
     res = {"opacity_coarse": torch.rand(n_o, generator=g)}
     if fine:
         res["opacity_fine"] = torch.rand(n_o, generator=g)
