@@ -843,7 +843,7 @@ def main():
     # size (coarse / fine pass), over the timed steps
     from nerf_pl_amd import functions as _functions
     backward_blocks = dict(skip_zero_gradient_samples=bool(_functions.ACTIVE_SAMPLES
-                                                           and math_main in ("f16x3", "bf16x6")))
+                                                           and math_main in _functions.ACTIVE_ARITHS))
     for k in ("mlp_bwd_dgrad", "mlp_bwd_dgrad_sigma"):
         evs = timer.events.get(k, [])
         if evs and any(ev[3] is not None for ev in evs):

@@ -132,8 +132,8 @@ int nr_wgrad_b1(const float* save, const float* grad_ws, int64_t n, float* works
                 float* grad_flat, void* stream);
 
 /* Training the sigma-only graph (models/rendering_shadows.py:167: every MLP
- * call of the shadow path is NeRF.forward(x, sigma_only=True)) on the split
- * arithmetics: nr_mlp_fwd_{x3,h3,b1} with sigma_only = 1 AND a save buffer
+ * call of the shadow path is NeRF.forward(x, sigma_only=True)), in every
+ * arithmetic: nr_mlp_fwd{,_x3,_h3,_b1} with sigma_only = 1 AND a save buffer
  * (ray path) runs layers 1-8 and the sigma head only, keeps the activations
  * those layers need and writes (n, 4) rows [0, 0, 0, sigma];
  * nr_mlp_bwd_sigma_* (g_out column 3 = d sigma, the rgb columns ignored)
@@ -141,6 +141,9 @@ int nr_wgrad_b1(const float* save, const float* grad_ws, int64_t n, float* works
  * computes the weight gradients of xyz_encoding_1..8 and the sigma head and
  * writes 0 for xyz_encoding_final, dir_encoding and rgb (not in the graph).
  * Contracts otherwise those of nr_mlp_bwd_* / nr_wgrad_*. */
+int nr_mlp_bwd_sigma(const float* packed_bwd, const float* head, const float* out,
+                     const float* g_out, const float* save, int64_t n, float* grad_ws,
+                     void* stream);
 int nr_mlp_bwd_sigma_x3(const void* packed_bwd, const float* head, const float* out,
                         const float* g_out, const float* save, int64_t n, float* grad_ws,
                         void* stream);
@@ -150,6 +153,8 @@ int nr_mlp_bwd_sigma_h3(const void* packed_bwd, const float* head, const float* 
 int nr_mlp_bwd_sigma_b1(const void* packed_bwd, const float* head, const float* out,
                         const float* g_out, const float* save, int64_t n, float* grad_ws,
                         void* stream);
+int nr_wgrad_sigma(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                   float* grad_flat, void* stream);
 int nr_wgrad_sigma_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
                       float* grad_flat, void* stream);
 int nr_wgrad_sigma_h3(const float* save, const float* grad_ws, int64_t n, float* workspace,
@@ -171,10 +176,22 @@ int nr_wgrad_sigma_b1(const float* save, const float* grad_ws, int64_t n, float*
  * feeds only nr_wgrad*_active with the same list, which gathers the saved
  * activations of samples[q]; the weight gradients equal the plain entry
  * points' up to the order of the split-K partial sums (a fixed order:
- * reproducible).  Split arithmetics (x3 = bf16x6, h3 = f16x3) only. */
+ * reproducible).  fp32 (no suffix), bf16x6 (x3) and f16x3 (h3); not the bf16
+ * variant (b1). */
 int64_t nr_active_scratch_ints(int64_t n);
 int nr_active_samples(const float* g_out, int64_t n, int32_t* samples, int32_t* count,
                       int32_t* scratch, void* stream);
+int nr_mlp_bwd_active(const float* packed_bwd, const float* head, const float* out,
+                      const float* g_out, const float* save, int64_t n, float* grad_ws,
+                      const int32_t* samples, const int32_t* count, void* stream);
+int nr_mlp_bwd_sigma_active(const float* packed_bwd, const float* head, const float* out,
+                            const float* g_out, const float* save, int64_t n, float* grad_ws,
+                            const int32_t* samples, const int32_t* count, void* stream);
+int nr_wgrad_active(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                    float* grad_flat, const int32_t* samples, const int32_t* count, void* stream);
+int nr_wgrad_sigma_active(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                          float* grad_flat, const int32_t* samples, const int32_t* count,
+                          void* stream);
 int nr_mlp_bwd_active_x3(const void* packed_bwd, const float* head, const float* out,
                          const float* g_out, const float* save, int64_t n, float* grad_ws,
                          const int32_t* samples, const int32_t* count, void* stream);

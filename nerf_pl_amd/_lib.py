@@ -62,6 +62,12 @@ SIGNATURES = {
     "nr_wgrad_sigma_active_x3": [_p, _p, _i64, _p, _p, _p, _p, _p],
     "nr_wgrad_sigma_active_h3": [_p, _p, _i64, _p, _p, _p, _p, _p],
     "nr_mlp_bwd": [_p, _p, _p, _p, _p, _i64, _p, _p],
+    "nr_mlp_bwd_sigma": [_p, _p, _p, _p, _p, _i64, _p, _p],
+    "nr_mlp_bwd_active": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_mlp_bwd_sigma_active": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_wgrad_sigma": [_p, _p, _i64, _p, _p, _p],
+    "nr_wgrad_active": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_wgrad_sigma_active": [_p, _p, _i64, _p, _p, _p, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
     "nr_sm_workspace_bytes": [_i64, _i64],
     "nr_wgrad": [_p, _p, _i64, _p, _p, _p],

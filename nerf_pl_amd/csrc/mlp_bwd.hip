@@ -36,18 +36,31 @@ struct BwdArgs {
     const float* save;
     int n;
     float* grad;
+    // optional (the *_active entry points, active.hip): the ascending list of
+    // the samples with a nonzero output gradient and its length m (device)
+    const int32_t* slist; const int32_t* scount;
 };
 
+// SO: the sigma-only graph (rendering_shadows.py:167, sigma_only=True): no rgb
+// head, dir layer or xyz_encoding_final, so the chain starts at d h8 =
+// W_sigma^T dsigma masked by h8 and streams the transposed weights from layer 8.
+// GA: over the packed sample list -- wave w takes positions 32w .. 32w+31, lane
+// (h, j) sample slist[32w + j], gathering its output rows and its ReLU mask
+// words (sample s keeps its bits in lanes s & 31 and 32 + (s & 31) of its
+// block, one uint4 per lane and layer: exactly the word this lane needs), and
+// writes every dz by position.  Positions past m carry zero gradients.
+template <bool SO, bool GA>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
-    const int blk = blockIdx.x * kWaves + wave;
+    const int blk = blockIdx.x * kWaves + wave;   // block of (packed) positions
     const int nb = (int)nr_blocks_pad(a.n);    // segment stride (padded)
-    if (blk >= (a.n + 31) / 32) return;         // no barriers in this kernel
+    const int m = GA ? __builtin_amdgcn_readfirstlane(*a.scount) : a.n;
+    if (blk >= (m + 31) / 32) return;           // no barriers in this kernel
     const int s_raw = blk * 32 + (lane & 31);
-    const bool valid = s_raw < a.n;
-    const int s = valid ? s_raw : a.n - 1;
+    const bool valid = s_raw < m;
+    const int s = GA ? a.slist[valid ? s_raw : m - 1] : (valid ? s_raw : a.n - 1);
     const float* PB = a.packed_bwd;
     const float* H = a.head;
     const float* SV = a.save;
@@ -58,9 +71,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     __shared__ __attribute__((aligned(16))) uint4 smask[kWaves][NR_MASK_LAYERS][64];
     {
         const uint4* gm = reinterpret_cast<const uint4*>(SV + nr_sv_mask(nb)) +
-                          (size_t)blk * NR_MASK_LAYERS * 64 + lane;
+                          (GA ? (size_t)(s >> 5) * NR_MASK_LAYERS * 64 + 32 * h + (s & 31)
+                              : (size_t)blk * NR_MASK_LAYERS * 64 + lane);
 #pragma unroll
-        for (int l = 0; l < NR_MASK_LAYERS; ++l)
+        for (int l = 0; l < (SO ? 8 : NR_MASK_LAYERS); ++l)   // SO: h1..h8, no hdir
             __builtin_amdgcn_global_load_lds(
                 (const void*)(gm + l * 64),
                 (__attribute__((address_space(3))) void*)&smask[wave][l][0], 16, 0, 0);
@@ -68,20 +82,39 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     const uint4* mask = &smask[wave][0][lane];   // [layer * 64]
 
     f32x4 wq[8];                 // weight group in flight across layer boundaries
-    nr_ld_first<8>(PB + NR_B_DIRT, lane, wq);
+    nr_ld_first<8>(PB + (SO ? NR_B_L8T : NR_B_DIRT), lane, wq);
     const f32x4 go = *reinterpret_cast<const f32x4*>(a.g_out + (size_t)s * 4);
     const f32x4 yo = *reinterpret_cast<const f32x4*>(a.out + (size_t)s * 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // masks landed in LDS (own wave only)
     // sigmoid backward: grad * (1 - y) * y  (ATen sigmoid_backward); tail lanes -> 0
+    // (the sigma-only graph has no rgb output)
     float dzr[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) dzr[c] = valid ? go[c] * (1.f - yo[c]) * yo[c] : 0.f;
+    for (int c = 0; c < 3; ++c) dzr[c] = valid && !SO ? go[c] * (1.f - yo[c]) * yo[c] : 0.f;
     const float dsig = valid ? go[3] : 0.f;
     if (h == 0) {
         f32x4 v = {dzr[0], dzr[1], dzr[2], dsig};
         *reinterpret_cast<f32x4*>(GD + nr_gd_dhead(nb) + ((size_t)blk * 32 + (lane & 31)) * 4) = v;
     }
 
+    f32x16 A[8], B[8];
+    // each layer's dz is written while the next backward layer runs (side hook)
+    auto dzseg = [&](int l) { return GD + nr_gd_dz(l, nb) + (size_t)blk * NR_NATIVE(256); };
+    auto side8 = [&](const f32x16 (&X)[8], float* dst) {
+        return [&X, dst, lane](int grp) { if (grp < 32) store_native_piece<8>(X, grp, dst, lane); };
+    };
+    if constexpr (SO) {
+        // d h8 = W_sigma^T dsigma, masked by h8
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(H + NR_H_WSIG + 32 * t + 8 * q + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) B[t][4 * q + e] = w[e] * dsig;
+            }
+        relu_mask<8>(B, mask[7 * 64]);
+    } else {
     // d hdir = W_rgb^T dz_rgb, masked by the dir-layer ReLU -> dz_dir (128)
     f32x16 C[4];
     {
@@ -103,12 +136,6 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
             }
     }
 
-    f32x16 A[8], B[8];
-    // each layer's dz is written while the next backward layer runs (side hook)
-    auto dzseg = [&](int l) { return GD + nr_gd_dz(l, nb) + (size_t)blk * NR_NATIVE(256); };
-    auto side8 = [&](const f32x16 (&X)[8], float* dst) {
-        return [&X, dst, lane](int grp) { if (grp < 32) store_native_piece<8>(X, grp, dst, lane); };
-    };
     // d feat = W_dir[:, :256]^T dz_dir   (xyz_encoding_final has no activation); stores dz_dir
     zero<8>(A);
     {
@@ -133,6 +160,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
                                [&](int g) { return A[g >> 4][g & 15]; }, side8(A, dzseg(8)));
         relu_mask<8>(B, mk);
     }
+    }   // !SO
 
 #define NR_BACK(DST, SRC, LOFF, NEXT, L)                                                     \
     {                                                                                         \
@@ -157,19 +185,59 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
 
 }  // namespace
 
+namespace {
+int bwd_launch(const char* name, bool so, const float* packed_bwd, const float* head,
+               const float* out, const float* g_out, const float* save, int64_t n,
+               float* grad_ws, const int32_t* slist, const int32_t* scount, void* stream) {
+    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "%s: n out of range", name);
+    if (n == 0) return 0;
+    NR_REQUIRE(packed_bwd && head && out && g_out && save && grad_ws, "%s: null pointer", name);
+    NR_REQUIRE((((uintptr_t)out | (uintptr_t)g_out | (uintptr_t)save | (uintptr_t)grad_ws |
+                 (uintptr_t)packed_bwd | (uintptr_t)head) & 15) == 0,
+               "%s: pointers must be 16-byte aligned", name);
+    BwdArgs a{packed_bwd, head, out, g_out, save, (int)n, grad_ws, slist, scount};
+    const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
+    hipStream_t st = (hipStream_t)stream;
+    if (so && slist) mlp_bwd_kernel<true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else if (so) mlp_bwd_kernel<true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else if (slist) mlp_bwd_kernel<false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else mlp_bwd_kernel<false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+    NR_LAUNCH_CHECK(name);
+    return 0;
+}
+}  // namespace
+
 NR_API int nr_mlp_bwd(const float* packed_bwd, const float* head, const float* out,
                       const float* g_out, const float* save, int64_t n, float* grad_ws,
                       void* stream) {
-    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_bwd: n out of range");
-    if (n == 0) return 0;
-    NR_REQUIRE(packed_bwd && head && out && g_out && save && grad_ws,
-               "nr_mlp_bwd: null pointer");
-    NR_REQUIRE((((uintptr_t)out | (uintptr_t)g_out | (uintptr_t)save | (uintptr_t)grad_ws |
-                 (uintptr_t)packed_bwd | (uintptr_t)head) & 15) == 0,
-               "nr_mlp_bwd: pointers must be 16-byte aligned");
-    BwdArgs a{packed_bwd, head, out, g_out, save, (int)n, grad_ws};
-    const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
-    mlp_bwd_kernel<<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
-    NR_LAUNCH_CHECK("nr_mlp_bwd");
-    return 0;
+    return bwd_launch("nr_mlp_bwd", false, packed_bwd, head, out, g_out, save, n, grad_ws,
+                      nullptr, nullptr, stream);
+}
+
+// the sigma-only graph (g_out column 3 = d sigma, the rgb columns ignored):
+// writes dz1..dz8 and the head gradient [0, 0, 0, dsigma] for nr_wgrad_sigma
+NR_API int nr_mlp_bwd_sigma(const float* packed_bwd, const float* head, const float* out,
+                            const float* g_out, const float* save, int64_t n, float* grad_ws,
+                            void* stream) {
+    return bwd_launch("nr_mlp_bwd_sigma", true, packed_bwd, head, out, g_out, save, n, grad_ws,
+                      nullptr, nullptr, stream);
+}
+
+// over the samples nr_active_samples listed: position q of every gradient
+// segment holds sample samples[q]'s rows; positions past *count are not read
+NR_API int nr_mlp_bwd_active(const float* packed_bwd, const float* head, const float* out,
+                             const float* g_out, const float* save, int64_t n, float* grad_ws,
+                             const int32_t* samples, const int32_t* count, void* stream) {
+    NR_REQUIRE(n == 0 || (samples && count), "nr_mlp_bwd_active: null sample list");
+    return bwd_launch("nr_mlp_bwd_active", false, packed_bwd, head, out, g_out, save, n, grad_ws,
+                      samples, count, stream);
+}
+
+NR_API int nr_mlp_bwd_sigma_active(const float* packed_bwd, const float* head, const float* out,
+                                   const float* g_out, const float* save, int64_t n,
+                                   float* grad_ws, const int32_t* samples, const int32_t* count,
+                                   void* stream) {
+    NR_REQUIRE(n == 0 || (samples && count), "nr_mlp_bwd_sigma_active: null sample list");
+    return bwd_launch("nr_mlp_bwd_sigma_active", true, packed_bwd, head, out, g_out, save, n,
+                      grad_ws, samples, count, stream);
 }

@@ -222,7 +222,20 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     // sigma = Linear(256, 1)(h8), raw (nerf.py:112)
     const float sigma = head_dot<8>(B, H + NR_H_WSIG, h) + H[NR_H_BSIG];
     if constexpr (SIGMA_ONLY) {
-        if (valid && h == 0) a.out[s] = sigma;
+        if (a.save != nullptr) {
+            // training a sigma-only graph (rendering_shadows.py:167): layers 1-8
+            // and the sigma head only; h8 and its ReLU mask saved where the full
+            // graph saves them, out rows (n, 4) [0, 0, 0, sigma] for the
+            // backward's contract (as mlp_fwd3.hip's sigma-only training forward)
+            if (save) {
+                store_native<8>(B, hseg(7), lane);
+                store_mask<8>(B, mseg(7), lane);
+            }
+            if (valid && h == 0)
+                *reinterpret_cast<f32x4*>(a.out + (size_t)s * 4) = f32x4{0.f, 0.f, 0.f, sigma};
+        } else if (valid && h == 0) {
+            a.out[s] = sigma;
+        }
         return;
     } else {
         // xyz_encoding_final: Linear(256,256), no activation (nerf.py:116); stores h8
@@ -283,6 +296,8 @@ NR_API int nr_mlp_fwd(const float* packed, const float* rays, const float* z, in
                    ((uintptr_t)save & 15) == 0,
                "nr_mlp_fwd: packed/out/save must be 16-byte aligned");
     const bool emb = x != nullptr;
+    NR_REQUIRE(!(sigma_only && save && emb),
+               "nr_mlp_fwd: a sigma_only run keeps activations only on the ray path");
     if (emb) {
         NR_REQUIRE(xstride >= (sigma_only ? NR_XYZ_CH : NR_XYZ_CH + NR_DIR_CH),
                    "nr_mlp_fwd: xstride %d too small", xstride);

@@ -148,7 +148,12 @@ struct SegGeo {
     }
 };
 
-template <int KA, int WA, int KB, int WB, int WM, int WN>
+// GAT: over the packed sample list (the fp32 *_active entry points): the
+// gradient operand is read by position, the input operand gathered -- the
+// float4 of column c of sample s sits at (s >> 5) * F4 + (e & ~31) + (s & 31) of
+// its block-native segment, so each thread resolves one sample per stage;
+// positions past m stage zeros
+template <int KA, int WA, int KB, int WB, int WM, int WN, bool GAT = false>
 __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int b0, int b1,
                                            float* lds, float* __restrict__ slab) {
     using GA = SegGeo<KA, WA>;
@@ -174,9 +179,17 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
     const bool ta = tid < GA::F4, tb = tid < GB::F4;
     const int ja = GA::j(tid), jb = GB::j(tid);
     f32x4 ra[GA::ITERS], rb[GB::ITERS];
+    const int m = wg_m(a);
     auto load = [&](int blk) {
         const f32x4* pa = reinterpret_cast<const f32x4*>(T.a.base) + (size_t)blk * GA::F4 + tid;
-        const f32x4* pb = reinterpret_cast<const f32x4*>(T.b.base) + (size_t)blk * GB::F4 + tid;
+        const f32x4* pb;
+        if constexpr (GAT) {
+            const int sj = a.slist[min(blk * 32 + jb, m - 1)];
+            pb = reinterpret_cast<const f32x4*>(T.b.base) + (size_t)(sj >> 5) * GB::F4 +
+                 (tid - jb) + (sj & 31);
+        } else {
+            pb = reinterpret_cast<const f32x4*>(T.b.base) + (size_t)blk * GB::F4 + tid;
+        }
 #pragma unroll
         for (int i = 0; i < GA::ITERS; ++i) if (ta) ra[i] = pa[kThreads * i];
 #pragma unroll
@@ -186,7 +199,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
     // float4; lanes are consecutive samples -> conflict-free); samples >= n of
     // the tail block become 0
     auto store = [&](int buf, int blk) {
-        const int nval = a.n - blk * 32;
+        const int nval = m - blk * 32;
         const bool ka = ja < nval, kb = jb < nval;
         float* la = lds + buf * kBuf + ja;
         float* lb = lds + buf * kBuf + kBufA + jb;
@@ -278,6 +291,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
     }
 }
 
+template <bool GA>
 __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[2 * kBuf];   // 144 KiB
     int t = 0;
@@ -293,17 +307,17 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     // (WM, WN) = wave grid over the task's output (<= 8 waves; 128 accumulators max)
     switch (__builtin_amdgcn_readfirstlane(T.id)) {
         case 0: case 4:
-            wgrad_body<SEG_ACC, 256, SEG_PE, 64, 8, 1>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 256, SEG_PE, 64, 8, 1, GA>(a, T, b0, b1, lds, slab); break;
         case 10:
-            wgrad_body<SEG_ACC, 128, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 128, SEG_ACC, 256, 2, 4, GA>(a, T, b0, b1, lds, slab); break;
         case 11:
-            wgrad_body<SEG_ACC, 128, SEG_DPE, 32, 4, 1>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 128, SEG_DPE, 32, 4, 1, GA>(a, T, b0, b1, lds, slab); break;
         case 12:
-            wgrad_body<SEG_HEAD, 4, SEG_ACC, 256, 1, 8>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_HEAD, 4, SEG_ACC, 256, 1, 8, GA>(a, T, b0, b1, lds, slab); break;
         case 13:
-            wgrad_body<SEG_HEAD, 4, SEG_ACC, 128, 1, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_HEAD, 4, SEG_ACC, 128, 1, 4, GA>(a, T, b0, b1, lds, slab); break;
         default:
-            wgrad_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4, GA>(a, T, b0, b1, lds, slab); break;
     }
 }
 
@@ -1396,7 +1410,8 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     else if (x3 && slist) wgrad3_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else if (x3 && !sigma_only) wgrad3_kernel<false, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else if (x3) wgrad3_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
-    else wgrad_kernel<<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (slist) wgrad_kernel<true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else wgrad_kernel<false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #endif
     NR_LAUNCH_CHECK("nr_wgrad");
     dim3 rg((256 * 256 + 256 + 255) / 256, kTasks);
@@ -1410,6 +1425,24 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
 NR_API int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
                     float* grad_flat, void* stream) {
     return wgrad_launch(false, false, save, grad_ws, n, workspace, grad_flat, stream);
+}
+// the exact-fp32 arithmetic's sigma-only and sample-list twins (as the split
+// arithmetics' below)
+NR_API int nr_wgrad_sigma(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                          float* grad_flat, void* stream) {
+    return wgrad_launch(false, true, save, grad_ws, n, workspace, grad_flat, stream);
+}
+NR_API int nr_wgrad_active(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                           float* grad_flat, const int32_t* samples, const int32_t* count,
+                           void* stream) {
+    NR_REQUIRE(samples && count, "nr_wgrad_active: null sample list");
+    return wgrad_launch(false, false, save, grad_ws, n, workspace, grad_flat, stream, samples, count);
+}
+NR_API int nr_wgrad_sigma_active(const float* save, const float* grad_ws, int64_t n,
+                                 float* workspace, float* grad_flat, const int32_t* samples,
+                                 const int32_t* count, void* stream) {
+    NR_REQUIRE(samples && count, "nr_wgrad_sigma_active: null sample list");
+    return wgrad_launch(false, true, save, grad_ws, n, workspace, grad_flat, stream, samples, count);
 }
 #endif
 

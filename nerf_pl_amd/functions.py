@@ -38,10 +38,13 @@ def _wgrad_workspace(device_index: int, stream: int = 0) -> torch.Tensor:
 # on the full kernels with a zero rgb gradient -- the A/B reference of the tests)
 SIGMA_TRAIN_KERNELS = os.environ.get("NERF_PL_AMD_SIGMA_TRAIN", "1") != "0"
 
-# the split arithmetics' backward works on the samples with a nonzero output
+# the backward works on the samples with a nonzero output
 # gradient only (nr_active_samples; exact: the others add zeros to every sum),
 # packed densely.  NERF_PL_AMD_ACTIVE_SAMPLES=0: every sample (the A/B reference)
 ACTIVE_SAMPLES = os.environ.get("NERF_PL_AMD_ACTIVE_SAMPLES", "1") != "0"
+# the arithmetics with *_active entry points (the bf16 variant keeps its
+# sample-major 16x16 bf16 chunks whole: no gather)
+ACTIVE_ARITHS = ("f16x3", "bf16x6", "fp32")
 # bench.py's kernel timer: a list every backward appends its (sample list
 # buffer, index of its length) to, so the rooflines count the samples worked on
 ACTIVE_LOG = None
@@ -65,11 +68,9 @@ class _FusedMLP(torch.autograd.Function):
                                       "pre-embedded input is not supported; use render_rays")
         packed_f, packed_b = model.packed(backward=train)
         # a sigma-only graph (rendering_shadows.py:167) trains through the
-        # sigma-only training kernels of the split arithmetics (layers 1-8 and
-        # the sigma head: no xyz_encoding_final / dir / rgb work),
-        # through the full kernels with a zero rgb gradient otherwise (fp32)
-        so_train = (train and sigma_only and SIGMA_TRAIN_KERNELS and x is None
-                    and ops.arith_of(packed_f) != "fp32")
+        # sigma-only training kernels (layers 1-8 and the sigma head: no
+        # xyz_encoding_final / dir / rgb work), in every arithmetic
+        so_train = train and sigma_only and SIGMA_TRAIN_KERNELS and x is None
         kern_sigma_only = sigma_only and (not train or so_train)
         out, save = ops.mlp_forward(packed_f, rays=rays, z=z, samples_per_ray=spr, x=x,
                                     sigma_only=kern_sigma_only, save=train)
@@ -95,7 +96,7 @@ class _FusedMLP(torch.autograd.Function):
         sfx = "_sigma" if ctx.so_kernels else ""
         st = stream_of(dev)
         active = ()
-        if ACTIVE_SAMPLES and ops.arith_of(packed_b) in ("f16x3", "bf16x6"):
+        if ACTIVE_SAMPLES and ops.arith_of(packed_b) in ACTIVE_ARITHS:
             # the samples with a nonzero output gradient, ascending (int32 [0, n)),
             # their count ([n]) and the compaction's scratch
             sl = torch.empty(n + 1 + 2 * ((n + 31) // 32), dtype=torch.int32, device=dev)

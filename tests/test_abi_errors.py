@@ -28,13 +28,13 @@ def _cases():
             (f"nr_wgrad{sfx}", [N, N, -1, N, N, N], NR_EINVAL),
             (f"nr_wgrad{sfx}", [N, N, 5, N, N, N], NR_EINVAL),
         ]
-        if sfx:
+        if True:       # every arithmetic has the sigma-only kernels (fp32 from round 4)
             c += [(f"nr_mlp_bwd_sigma{sfx}", [N, N, N, N, N, -1, N, N], NR_EINVAL),
                   (f"nr_mlp_bwd_sigma{sfx}", [N, N, N, N, N, 0, N, N], 0),
                   (f"nr_mlp_bwd_sigma{sfx}", [N, N, N, N, N, 5, N, N], NR_EINVAL),
                   (f"nr_wgrad_sigma{sfx}", [N, N, -1, N, N, N], NR_EINVAL),
                   (f"nr_wgrad_sigma{sfx}", [N, N, 5, N, N, N], NR_EINVAL)]
-        if sfx in ("_x3", "_h3"):     # zero-gradient sample lists (split arithmetics)
+        if sfx in ("", "_x3", "_h3"):     # zero-gradient sample lists (not the bf16 variant)
             for so in ("", "_sigma"):
                 c += [(f"nr_mlp_bwd{so}_active{sfx}", [N, N, N, N, N, -1, N, N, N, N], NR_EINVAL),
                       (f"nr_mlp_bwd{so}_active{sfx}", [N, N, N, N, N, 5, N, N, N, N], NR_EINVAL),

@@ -1,4 +1,5 @@
-"""Zero-gradient samples: the split arithmetics' backward works
+"""Zero-gradient samples: the backward (f16x3, bf16x6 and, from
+round 4, exact fp32) works
 on the samples with a nonzero output gradient only, packed densely
 (``nr_active_samples`` + the ``*_active`` data- and weight-gradient entry
 points, which gather the saved activations of the listed samples).  A sample
@@ -107,7 +108,7 @@ def _zeroed(kind):
 CASES = ("dense", "scattered", "blocks", "runs", "one", "none")
 
 
-@pytest.mark.parametrize("math", ["f16x3", "bf16x6"])
+@pytest.mark.parametrize("math", ["f16x3", "bf16x6", "fp32"])
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("sigma_only", [False, True])
 def test_active_backward_matches_every_sample(math, case, sigma_only, monkeypatch):

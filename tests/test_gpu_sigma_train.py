@@ -1,6 +1,6 @@
 """Sigma-only training kernels: the shadow path trains the
 sigma-only graph (models/rendering_shadows.py:167, NeRF.forward(x,
-sigma_only=True) on every call), which the split arithmetics run on dedicated
+sigma_only=True) on every call), which every arithmetic (fp32 from round 4) runs on dedicated
 kernels -- layers 1-8 and the sigma head only -- instead of the full kernels
 with a zero rgb gradient.  Both must give the same step: the forward bit for
 bit (the same sums), every gradient within 1e-6 normwise (only the sigma
@@ -46,7 +46,7 @@ def _step(math, so_kernels, monkeypatch, n=700, seed=3):
               for name, p in m.named_parameters()] for m in models])
 
 
-@pytest.mark.parametrize("math", ["f16x3", "bf16x6", "bf16"])
+@pytest.mark.parametrize("math", ["f16x3", "bf16x6", "bf16", "fp32"])
 def test_sigma_only_training_kernels_match_full_kernels(math, monkeypatch):
     out_a, grads_a = _step(math, True, monkeypatch)
     out_b, grads_b = _step(math, False, monkeypatch)
