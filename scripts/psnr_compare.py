@@ -153,7 +153,7 @@ def main():
     train, train_rgb, test, test_rgb = scene()
     if args.draw_seeds:
         # several runs in one process (the scene's ground truth is built once);
-        # one JSON per seed under --out-dir, named like scripts/psnr_r03.sh's
+        # one JSON per seed under --out-dir, named like scripts/psnr.sh's
         seeds = []
         for part in args.draw_seeds.split(","):     # "lo-hi" ranges, comma-separated
             lo, _, hi = part.partition("-")

@@ -1,0 +1,179 @@
+"""BASELINE.json configs[3] at its own size and shape: Blender lego 800x800,
+64 coarse + 128 fine, rays sharded over 8 ranks (the Lightning DDP path,
+train.py:167-178, whose DistributedSampler gives rank r perm[r::world] of the
+shuffled pixel pool -- nerf_pl_amd.rays.RaySampler).  One rank's 4,096-ray
+batch of the 100-pose orbit (64M rays in the pool) is drawn exactly as
+bench.py --config cfg4 draws it on rank 5 of 8, generated on the device, and
+checked against the CPU oracle (the reference's algorithm, pinned to the
+reference by tests/golden) with the reference's random draws replayed:
+
+* the rays themselves against the host restatement of get_ray_directions /
+  get_rays (datasets/ray_utils.py) at 2e-6;
+* render_rays' every output at 1e-4 (depths relative), coarse weights at
+  1e-4, every ray whose fine depths moved explained by a sample_pdf knot flip
+  (tests/screening.py);
+* the training step's parameter gradients (MSE coarse + fine against the
+  batch's target colours, train.py:107) on a 1,024-ray share of the batch,
+  each tensor within max(1e-4, the oracle's own fp32-vs-float64 distance) of
+  the fp32 oracle, as tests/test_gpu_random.py.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+from screening import pdf_flips
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+IMG, POSES, S, I, B = 800, 100, 64, 128, 4096
+RANK, WORLD = 5, 8
+
+
+def _batch():
+    """rank RANK's first batch of bench.py --config cfg4 (same poses, pool,
+    sampler seed and partition)"""
+    from nerf_pl_amd.rays import RaySampler, blender_focal, generate_rays, pose_spherical
+    poses = torch.stack([pose_spherical(-180.0 + 360.0 * k / POSES, -30.0, 4.0)
+                         for k in range(POSES)])
+    focal = blender_focal(IMG)
+    torch.manual_seed(1234)
+    pool_rgb = torch.rand(POSES * IMG * IMG, 3, device=DEV)
+    sampler = RaySampler(poses.to(DEV), IMG, IMG, focal, 1.0, 200.0, rgb_pool=pool_rgb, seed=99,
+                         rank=RANK, world=WORLD)
+    sel = sampler.next_indices(B)
+    rays, rgbs = generate_rays(poses.to(DEV), IMG, IMG, focal, 1.0, 200.0, sel, rgb_pool=pool_rgb)
+    return poses, focal, sel.cpu(), rays.cpu(), rgbs.cpu()
+
+
+def _draws(n, seed=17):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.rand(n, S, generator=g), torch.randn(n, S, generator=g),
+            torch.rand(n, I, generator=g), torch.rand(n, I, generator=g),
+            torch.randn(n, S + I, generator=g)]
+
+
+def _params(dt=torch.float32, grad=False):
+    return [{k: v.to(dt).requires_grad_(grad) for k, v in O.make_params(s, sigma_bias=0.5).items()}
+            for s in (31, 32)]
+
+
+def _models():
+    from nerf_pl_amd import NeRF
+    out = []
+    for p in _params():
+        m = NeRF()
+        m.load_state_dict(p)
+        out.append(m.to(DEV))
+    return out
+
+
+def _ours(models, rays, draws, cap=None):
+    from nerf_pl_amd import Embedding, ReplayRNG, render_rays
+    return render_rays(models, [Embedding(3, 10), Embedding(3, 4)], rays.to(DEV), S, False, 1.0,
+                       1.0, I, 32768, False, rng=ReplayRNG(draws), _capture=cap)
+
+
+def _screen(cap, ocap, draws):
+    zf = cap["z_fine"].detach().cpu().numpy()
+    ozf = ocap["z_fine"].detach().numpy()
+    bad = np.abs(zf - ozf).max(1) > 1e-4 * np.maximum(1, np.abs(zf).max(1))
+    moved, explained = pdf_flips(cap["z_fine"], {k: v.detach() for k, v in ocap.items()},
+                                 draws[-3])
+    assert not (bad & ~moved).any(), "z_fine differs although every importance depth matches"
+    assert not (moved & ~explained).any(), \
+        f"z_fine moved away from any CDF knot: rays {np.nonzero(moved & ~explained)[0][:8]}"
+    return bad
+
+
+def test_cfg4_rank_batch_rays():
+    from nerf_pl_amd.rays import get_ray_directions, get_rays
+    poses, focal, sel, rays, _ = _batch()
+    assert rays.shape == (B, 8) and len(set(sel.tolist())) == B
+    # rank r's share of the epoch: perm[r::world] of one permutation of all pixels
+    assert int(sel.max()) < POSES * IMG * IMG
+    dirs = get_ray_directions(IMG, IMG, focal).reshape(-1, 3)
+    pose, pix = sel // (IMG * IMG), sel % (IMG * IMG)
+    for k in torch.unique(pose).tolist():
+        idx = torch.nonzero(pose == k).flatten()
+        o, d = get_rays(dirs[pix[idx]], poses[k])
+        torch.testing.assert_close(rays[idx, :3], o, rtol=0, atol=2e-6)
+        torch.testing.assert_close(rays[idx, 3:6], d, rtol=0, atol=2e-6)
+    assert (rays[:, 6] == 1.0).all() and (rays[:, 7] == 200.0).all()
+
+
+def test_cfg4_rank_batch_matches_oracle():
+    torch.set_num_threads(16)
+    _, _, _, rays, _ = _batch()
+    draws = _draws(B)
+    cap, ocap = {}, {}
+    with torch.no_grad():
+        res = _ours(_models(), rays, draws, cap)
+        ref = O.render_rays(_params(), rays, S, False, 1.0, 1.0, I, 32768, False,
+                            rng=O.ReplayRNG(draws), capture=ocap)
+    bad = _screen(cap, ocap, draws)
+    assert bad.mean() <= 0.01, f"{bad.sum()} rays with a sample_pdf bin flip"
+    assert sorted(res) == sorted(ref)
+    for k in ref:
+        got, exp = res[k].cpu().numpy(), ref[k].numpy()
+        assert got.shape == exp.shape, k
+        err = np.abs(got - exp)
+        if k.startswith("depth"):
+            err = err / np.maximum(1.0, np.abs(exp))
+        err = err.reshape(err.shape[0], -1).max(1)
+        ok = (err <= 1e-4) | bad
+        assert ok.all(), f"{k}: max err {err[~bad].max():.3g} on {int((~ok).sum())} rays"
+    w = cap["weights_coarse"].cpu().numpy()
+    assert np.abs(w - ocap["weights_coarse"].numpy()).max() <= 1e-4
+    print(f"cfg4 rank batch: {int(bad.sum())} of {B} rays screened (sample_pdf knot flips)")
+
+
+def _loss(out, tgt, keep):
+    """losses.py MSELoss (coarse + fine) over the kept rays"""
+    k = keep.to(out["rgb_coarse"].device, out["rgb_coarse"].dtype).view(-1, 1)
+    t = tgt.to(out["rgb_coarse"].device, out["rgb_coarse"].dtype)
+    n = k.sum() * 3
+    return (((out["rgb_coarse"] - t) ** 2) * k).sum() / n + (((out["rgb_fine"] - t) ** 2) * k).sum() / n
+
+
+@pytest.mark.parametrize("math_", ["f16x3", "fp32"])
+def test_cfg4_training_step_gradients_match_oracle(math_, monkeypatch):
+    from nerf_pl_amd import ops
+    monkeypatch.setattr(ops, "MATH", math_)
+    torch.set_num_threads(16)
+    n = 1024
+    _, _, _, rays, rgbs = _batch()
+    rays, rgbs = rays[:n].contiguous(), rgbs[:n]
+    draws = _draws(B)
+    draws = [d[:n] for d in draws]
+    models = _models()
+    cap = {}
+    res = _ours(models, rays, draws, cap)
+    p32, p64 = _params(grad=True), _params(torch.float64, grad=True)
+    c32, c64 = {}, {}
+    ref = O.render_rays(p32, rays, S, False, 1.0, 1.0, I, 32768, False, rng=O.ReplayRNG(draws),
+                        capture=c32)
+    ref64 = O.render_rays(p64, rays.double(), S, False, 1.0, 1.0, I, 32768, False,
+                          rng=O.ReplayRNG([d.double() for d in draws]), capture=c64)
+    bad = _screen(cap, c32, draws)
+    z32, z64 = c32["z_fine"].detach().double(), c64["z_fine"].detach()
+    bad |= ((z32 - z64).abs().max(1).values > 1e-4 * z64.abs().max(1).values.clamp(min=1)).numpy()
+    assert bad.mean() <= 0.02, f"{bad.sum()} rays screened"
+    keep = torch.from_numpy(~bad)
+    _loss(res, rgbs, keep).backward()
+    _loss(ref, rgbs, keep).backward()
+    _loss(ref64, rgbs, keep).backward()
+    worst = 0.0
+    for m, p, q in zip(models, p32, p64):
+        for name, w in m.named_parameters():
+            exp, e64 = p[name].grad.double(), q[name].grad
+            got = w.grad.detach().cpu().double()
+            scale = exp.norm() + 1e-30
+            bound = max(1e-4, ((exp - e64).norm() / scale).item())
+            dev = ((got - exp).norm() / scale).item()
+            worst = max(worst, dev / bound)
+            assert dev <= bound, f"{math_} {name}: normwise deviation {dev:.3g} > {bound:.3g}"
+    assert math.isfinite(worst)
+    print(f"cfg4 {math_} gradients: worst deviation {worst:.2f} of its bound")
