@@ -91,6 +91,7 @@ __device__ __forceinline__ void report_max(float m, float* slot, int lane) {
 template <int NF, bool MASK>
 struct GradU {
     static constexpr bool kStores = true;
+    static constexpr bool kPaired = false;
     const f32x4 (&X)[NF][2];
     float* dst;
     uint32_t mw[4];

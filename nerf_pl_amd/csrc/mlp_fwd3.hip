@@ -204,6 +204,7 @@ struct Fwd3Args {
 template <bool RELU, bool STORE, bool MASK, bool SIG, bool ROWS = true>
 struct AccU {
     static constexpr bool kStores = STORE;
+    static constexpr bool kPaired = STORE && ROWS && kRowPair;
     template <typename P> __device__ __forceinline__ void begin(const P&) {}
     const f32x4 (&X)[16][2];
     float* dst;
@@ -211,6 +212,7 @@ struct AccU {
     const float* wsig;
     int lane, g;
     float pend[2] = {0.f, 0.f};
+    f32x4 held = {0.f, 0.f, 0.f, 0.f};   // kPaired: the even tile, stored with the odd one
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     float sig[2] = {0.f, 0.f};
     template <typename SC>
@@ -233,8 +235,14 @@ struct AccU {
             } else {
                 const int F = 2 * s + (p >> 1);
                 const f32x4 v = {pend[0], pend[1], x0, x1};
-                if constexpr (ROWS) store_row<256>(v, F, sb, dst, lane);
-                else store_n16(v, F, sb, dst, lane);
+                if constexpr (kPaired) {
+                    if (p == 1) held = v;
+                    else store_row_pair<256>(held, v, 2 * s, sb, dst, lane);
+                } else if constexpr (ROWS) {
+                    store_row<256>(v, F, sb, dst, lane);
+                } else {
+                    store_n16(v, F, sb, dst, lane);
+                }
                 if constexpr (MASK) {
                     mask_bits(v, F, sb, w);
                     if (s == 7 && sb == 1 && p == 3)
@@ -249,6 +257,7 @@ struct AccU {
 template <int N>
 struct PeU {
     static constexpr bool kStores = false;
+    static constexpr bool kPaired = false;
     template <typename P> __device__ __forceinline__ void begin(const P&) {}
     const float (&pe)[2][N];
     template <typename SC>

@@ -465,6 +465,7 @@ __device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][
 // getter that fed this layer (the producer) has split all of its units.
 struct NoNext {
     static constexpr bool kStores = false;
+    static constexpr bool kPaired = false;
     template <typename P> __device__ __forceinline__ void begin(const P&) {}
     template <typename T> __device__ __forceinline__ void operator()(T, int, int, float& x0, float& x1) const {
         x0 = x1 = 0.f;
@@ -508,12 +509,18 @@ __host__ __device__ constexpr int unit_at(int t) {
     if constexpr (NH == 1) return t;
     else return t >= 3 && t <= 6 ? 4 * HF + t - 3 : -1;
 }
-// stores a storing getter issues before tile 7 of its group (one per odd unit)
-template <int NH, int HF>
+// stores a storing getter issues before tile 7 of its group: one per odd unit,
+// or (PAIRED: the two halves of a 128-B row line together, x3.h store_row_pair)
+// two per unit p = 3
+template <int NH, int HF, bool PAIRED = false>
 __host__ __device__ constexpr int stores_before7() {
     int n = 0;
-    for (int t = 0; t < kTiles - 1; ++t)
-        if (unit_at<NH, HF>(t) >= 0 && (unit_at<NH, HF>(t) & 1)) ++n;
+    for (int t = 0; t < kTiles - 1; ++t) {
+        const int u = unit_at<NH, HF>(t);
+        if (u < 0) continue;
+        if (PAIRED) n += (u & 3) == 3 ? 2 : 0;
+        else n += u & 1;
+    }
     return n;
 }
 
@@ -537,7 +544,8 @@ __device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)
             side(IC<NH * S + HF>(), t);
         };
         constexpr bool ust = S + 1 < KS ? GetU::kStores : NextU::kStores;
-        constexpr int extra = (ust ? stores_before7<NH, HF>() : 0) + Side::kBefore7;
+        constexpr bool upr = S + 1 < KS ? GetU::kPaired : NextU::kPaired;
+        constexpr int extra = (ust ? stores_before7<NH, HF, upr>() : 0) + Side::kBefore7;
         group_mm<TAB, Q, QEND, 8 * HF, INIT && S == 0, extra>(dma.ring, lane, acc, b, cinit, hook, f0);
         seg_group<TAB, Q0, S, KS, NH, QEND, INIT, HF + 1>(dma, lane, acc, getu, nextu, cinit, side,
                                                           b, bn, f0);
@@ -680,6 +688,52 @@ __device__ __forceinline__ void store_row(const f32x4& v, int F, int S, float* _
 #else
     *p = v;
 #endif
+#endif
+}
+
+// NR_ROW_PAIR (A/B knob for the row stores of the full graph's forward):
+// 0 = each 64-B half of a sample's 128-B row line stored as soon as its tile is
+// split (two units apart); 1 = both halves stored back to back; 2 = whole
+// lines: the odd tile's values rotated by 8 lanes within each 16-lane row
+// (DPP row_ror:8 with bank masks, no other VALU), so that one store writes 8
+// samples x 128 B -- full lines instead of the partial 64-B segments that
+// made the forward write 1.30x its bytes (round-3 PMC)
+#ifndef NR_ROW_PAIR
+#define NR_ROW_PAIR 0
+#endif
+constexpr bool kRowPair = NR_ROW_PAIR != 0 && !NR_BF1;
+
+// tiles F0 (even) and F0 + 1 of sample tile S: the 128-B row line [16 F0, 16 F0 + 32)
+template <int W>
+__device__ __forceinline__ void store_row_pair(const f32x4& t0, const f32x4& t1, int F0, int S,
+                                               float* __restrict__ blk, int lane) {
+#if NR_ROW_PAIR == 2
+    // lane (g, j): A = samples 16S + (j & 7), B = samples 16S + 8 + (j & 7);
+    // in A lanes j < 8 write their own tile F0, lanes j >= 8 tile F0 + 1 of
+    // lane j - 8; in B the other way round
+    const int j = lane & 15, g = lane >> 4;
+    f32x4 a, b;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int o = __float_as_int(t0[r]), s1 = __float_as_int(t1[r]);
+        a[r] = __int_as_float(__builtin_amdgcn_update_dpp(o, s1, 0x128, 0xF, 0xC, false));
+        b[r] = __int_as_float(__builtin_amdgcn_update_dpp(o, s1, 0x128, 0xF, 0x3, false));
+    }
+    const int hi = j >> 3;
+    f32x4* pa = reinterpret_cast<f32x4*>(blk + (16 * S + (j & 7)) * W + 16 * F0 + 16 * hi + 4 * g);
+    f32x4* pb = reinterpret_cast<f32x4*>(blk + (16 * S + 8 + (j & 7)) * W + 16 * F0 + 16 * (1 - hi) + 4 * g);
+#if NR_X3_DBG == 9
+    asm volatile("" ::"v"(a), "v"(b), "v"(pa), "v"(pb));
+#elif NR_NT_STORE && NR_ROW_NT
+    __builtin_nontemporal_store(a, pa);
+    __builtin_nontemporal_store(b, pb);
+#else
+    *pa = a;
+    *pb = b;
+#endif
+#else
+    store_row<W>(t0, F0, S, blk, lane);
+    store_row<W>(t1, F0 + 1, S, blk, lane);
 #endif
 }
 
