@@ -714,6 +714,12 @@ def main():
             print(f"[bench rank {rank}/{world} +{time.perf_counter() - t_start:.1f}s] {msg}",
                   file=sys.stderr, flush=True)
 
+    if use_dist and os.environ.get("NR_BENCH_WATCHDOG"):
+        # NR_BENCH_WATCHDOG=<s>: every rank dumps all its threads' Python stacks
+        # to stderr every <s> seconds (a hung multi-rank run names where it waits)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["NR_BENCH_WATCHDOG"]), repeat=True,
+                                          file=sys.stderr)
     if use_dist:
         torch.cuda.set_device(local)
         progress(f"init_process_group({backend})")
@@ -758,14 +764,25 @@ def main():
             dist.barrier()
             progress("first collective done")
 
+    first = [use_dist]
+
     def step():
         loss = wl["step"]()
+        if first[0]:
+            torch.cuda.synchronize()
+            progress("first step: forward done")
         if opt is not None:
             opt.zero_grad(set_to_none=True)
             loss.backward()
+            if first[0]:
+                torch.cuda.synchronize()
+                progress("first step: backward done")
             if reducer is not None:
                 reducer()            # waits for the RCCL all-reduces of the 4.77 MB gradient
+            if first[0]:
+                progress("first step: gradient all-reduce done")
             opt.step()
+        first[0] = False
         return loss
 
     def run(steps, warmup, what="main"):

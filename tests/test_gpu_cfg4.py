@@ -13,9 +13,15 @@ reference by tests/golden) with the reference's random draws replayed:
   1e-4, every ray whose fine depths moved explained by a sample_pdf knot flip
   (tests/screening.py);
 * the training step's parameter gradients (MSE coarse + fine against the
-  batch's target colours, train.py:107) on a 1,024-ray share of the batch,
-  each tensor within max(1e-4, the oracle's own fp32-vs-float64 distance) of
-  the fp32 oracle, as tests/test_gpu_random.py.
+  batch's target colours, train.py:107) on a 1,024-ray share of the batch.
+  The reference's own fp32 gradient sits a distance `floor` from the float64
+  truth (the oracle evaluated in float64; near/far 1/200 and the 2^9
+  positional-encoding frequency make the step ill-conditioned), so two
+  fp32-accurate evaluations can sit up to ~sqrt(2) floor apart: each tensor
+  must be within max(1e-4, sqrt(2) floor) of the fp32 oracle, or at least as
+  close to the float64 truth as the reference's fp32 is (max(1e-4, floor)).
+  Measured on the first run: the exact-fp32 sigma head sat 1.5e-4 from the
+  fp32 oracle but 6.9e-5 from float64, where the oracle's fp32 sits ~9e-5.
 """
 import math
 
@@ -170,10 +176,14 @@ def test_cfg4_training_step_gradients_match_oracle(math_, monkeypatch):
         for name, w in m.named_parameters():
             exp, e64 = p[name].grad.double(), q[name].grad
             got = w.grad.detach().cpu().double()
-            scale = exp.norm() + 1e-30
-            bound = max(1e-4, ((exp - e64).norm() / scale).item())
+            scale, s64 = exp.norm() + 1e-30, e64.norm() + 1e-30
+            floor = ((exp - e64).norm() / s64).item()
+            bound = max(1e-4, math.sqrt(2) * floor)
             dev = ((got - exp).norm() / scale).item()
-            worst = max(worst, dev / bound)
-            assert dev <= bound, f"{math_} {name}: normwise deviation {dev:.3g} > {bound:.3g}"
+            dev64 = ((got - e64).norm() / s64).item()
+            ok = dev <= bound or dev64 <= max(1e-4, floor)
+            worst = max(worst, min(dev / bound, dev64 / max(1e-4, floor)))
+            assert ok, (f"{math_} {name}: {dev:.3g} from the fp32 oracle (bound {bound:.3g}), "
+                        f"{dev64:.3g} from float64 (reference fp32: {floor:.3g})")
     assert math.isfinite(worst)
     print(f"cfg4 {math_} gradients: worst deviation {worst:.2f} of its bound")
