@@ -83,6 +83,8 @@ FLOP_DGRAD_SIGMA = FLOP_FWD_SIGMA - 2 * 2 * 63 * 256             # 918,016
 BYTES_WGRAD_SIGMA = 4 * (64 + 8 * 256 + 8 * 256 + 4)             # 16,656
 KERNEL_FLOP = {"mlp_fwd": FLOP_FWD, "mlp_fwd_sigma": FLOP_FWD_SIGMA,
                "mlp_fwd_sigma_train": FLOP_FWD_SIGMA,
+               # the deferred save's re-run over the listed samples (functions.DEFER_SAVE)
+               "mlp_fwd_listed": FLOP_FWD, "mlp_fwd_sigma_listed": FLOP_FWD_SIGMA,
                "mlp_bwd_dgrad": FLOP_DGRAD, "mlp_bwd_dgrad_sigma": FLOP_DGRAD_SIGMA,
                "mlp_wgrad": FLOP_WGRAD, "mlp_wgrad_sigma": FLOP_FWD_SIGMA}
 CONFIGS = ("cfg2", "cfg3", "cfg4", "cfg5", "eval")
@@ -279,7 +281,9 @@ def install_timers(timer):
 
     def call_tag(name, *a):
         base = name[:-3] if name[-3:] in ("_x3", "_h3", "_b1") else name
-        base = base[:-7] if base.endswith("_active") else base
+        base = base[:-7] if base.endswith(("_active", "_listed")) else base
+        if name.startswith("nr_mlp_fwd_listed"):   # a[5]: sigma_only
+            return ("mlp_fwd_sigma_listed" if a[5] else "mlp_fwd_listed"), int(a[3])
         if base == "nr_mlp_fwd":
             if a[7]:     # sigma_only: inference, or the sigma-only training forward (save)
                 return ("mlp_fwd_sigma_train" if a[9] else "mlp_fwd_sigma"), int(a[3])
@@ -305,7 +309,8 @@ def install_timers(timer):
             return orig_call(name, *a)
         tag, n = call_tag(name, *a)
         # a *_active backward entry: the block list functions.py just built
-        act = F.ACTIVE_LOG[-1] if "_active" in name and F.ACTIVE_LOG else None
+        act = F.ACTIVE_LOG[-1] if ("_active" in name or "_listed" in name) and F.ACTIVE_LOG \
+            else None
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()

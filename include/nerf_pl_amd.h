@@ -215,6 +215,62 @@ int nr_wgrad_sigma_active_h3(const float* save, const float* grad_ws, int64_t n,
                              float* grad_flat, const int32_t* samples, const int32_t* count,
                              void* stream);
 
+/* Deferred save.  A training forward whose backward lists few
+ * samples (the sigma-only graphs of the shadow path: ~0.1% of a light image's
+ * samples, ~20% of the camera rays') runs as inference (nr_mlp_fwd* without a
+ * save buffer); its backward lists the samples (nr_active_samples), then
+ * nr_mlp_fwd_listed* re-evaluates the training forward for samples[q],
+ * q < *count only -- the same layers bit for bit -- saving their activations
+ * by POSITION q into save (sized for n samples, nr_layout_query(3) per block,
+ * as nr_mlp_fwd's; sigma_only selects the sigma-only graph), and no output.
+ * nr_mlp_bwd[_sigma]_listed* / nr_wgrad[_sigma]_listed* are the data and
+ * weight gradients over those positions (g_out / out rows gathered by the
+ * list): the same sums, in the same split-K order, as the *_active entry
+ * points over a forward-time save.  fp32 (no suffix), bf16x6 (_x3), f16x3
+ * (_h3). */
+int nr_mlp_fwd_listed(const float* packed, const float* rays, const float* z, int64_t n,
+                      int samples_per_ray, int sigma_only, float* save, const int32_t* samples,
+                      const int32_t* count, void* stream);
+int nr_mlp_fwd_listed_x3(const void* packed, const float* rays, const float* z, int64_t n,
+                         int samples_per_ray, int sigma_only, float* save, const int32_t* samples,
+                         const int32_t* count, void* stream);
+int nr_mlp_fwd_listed_h3(const void* packed, const float* rays, const float* z, int64_t n,
+                         int samples_per_ray, int sigma_only, float* save, const int32_t* samples,
+                         const int32_t* count, void* stream);
+int nr_mlp_bwd_listed(const float* packed_bwd, const float* head, const float* out,
+                      const float* g_out, const float* save, int64_t n, float* grad_ws,
+                      const int32_t* samples, const int32_t* count, void* stream);
+int nr_mlp_bwd_listed_x3(const void* packed_bwd, const float* head, const float* out,
+                         const float* g_out, const float* save, int64_t n, float* grad_ws,
+                         const int32_t* samples, const int32_t* count, void* stream);
+int nr_mlp_bwd_listed_h3(const void* packed_bwd, const float* head, const float* out,
+                         const float* g_out, const float* save, int64_t n, float* grad_ws,
+                         const int32_t* samples, const int32_t* count, void* stream);
+int nr_mlp_bwd_sigma_listed(const float* packed_bwd, const float* head, const float* out,
+                            const float* g_out, const float* save, int64_t n, float* grad_ws,
+                            const int32_t* samples, const int32_t* count, void* stream);
+int nr_mlp_bwd_sigma_listed_x3(const void* packed_bwd, const float* head, const float* out,
+                               const float* g_out, const float* save, int64_t n, float* grad_ws,
+                               const int32_t* samples, const int32_t* count, void* stream);
+int nr_mlp_bwd_sigma_listed_h3(const void* packed_bwd, const float* head, const float* out,
+                               const float* g_out, const float* save, int64_t n, float* grad_ws,
+                               const int32_t* samples, const int32_t* count, void* stream);
+int nr_wgrad_listed(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                    float* grad_flat, const int32_t* samples, const int32_t* count, void* stream);
+int nr_wgrad_listed_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                       float* grad_flat, const int32_t* samples, const int32_t* count, void* stream);
+int nr_wgrad_listed_h3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                       float* grad_flat, const int32_t* samples, const int32_t* count, void* stream);
+int nr_wgrad_sigma_listed(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                          float* grad_flat, const int32_t* samples, const int32_t* count,
+                          void* stream);
+int nr_wgrad_sigma_listed_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                             float* grad_flat, const int32_t* samples, const int32_t* count,
+                             void* stream);
+int nr_wgrad_sigma_listed_h3(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                             float* grad_flat, const int32_t* samples, const int32_t* count,
+                             void* stream);
+
 /* Dense sigma query (extract_color_mesh.py:114-137, the marching-cubes grid):
  * sigma_out (n) = NeRF sigma head at points pts (n,3) -- the sigma-only fused
  * kernel with the positional encoding computed in-kernel (sigma does not

@@ -68,6 +68,21 @@ SIGNATURES = {
     "nr_wgrad_sigma": [_p, _p, _i64, _p, _p, _p],
     "nr_wgrad_active": [_p, _p, _i64, _p, _p, _p, _p, _p],
     "nr_wgrad_sigma_active": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_mlp_fwd_listed": [_p, _p, _p, _i64, _i, _i, _p, _p, _p, _p],
+    "nr_mlp_bwd_listed": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_mlp_bwd_sigma_listed": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_wgrad_listed": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_wgrad_sigma_listed": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_mlp_fwd_listed_x3": [_p, _p, _p, _i64, _i, _i, _p, _p, _p, _p],
+    "nr_mlp_bwd_listed_x3": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_mlp_bwd_sigma_listed_x3": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_wgrad_listed_x3": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_wgrad_sigma_listed_x3": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_mlp_fwd_listed_h3": [_p, _p, _p, _i64, _i, _i, _p, _p, _p, _p],
+    "nr_mlp_bwd_listed_h3": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_mlp_bwd_sigma_listed_h3": [_p, _p, _p, _p, _p, _i64, _p, _p, _p, _p],
+    "nr_wgrad_listed_h3": [_p, _p, _i64, _p, _p, _p, _p, _p],
+    "nr_wgrad_sigma_listed_h3": [_p, _p, _i64, _p, _p, _p, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
     "nr_sm_workspace_bytes": [_i64, _i64],
     "nr_wgrad": [_p, _p, _i64, _p, _p, _p],

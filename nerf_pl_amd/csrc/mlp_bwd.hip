@@ -49,8 +49,12 @@ struct BwdArgs {
 // words (sample s keeps its bits in lanes s & 31 and 32 + (s & 31) of its
 // block, one uint4 per lane and layer: exactly the word this lane needs), and
 // writes every dz by position.  Positions past m carry zero gradients.
-template <bool SO, bool GA>
+// GM = 2: the same list over a save buffer written by position
+// (nr_mlp_fwd_listed, the deferred save): masks by position, only the output
+// rows gathered
+template <bool SO, int GM>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
+    constexpr bool GA = GM != 0;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
@@ -71,8 +75,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     __shared__ __attribute__((aligned(16))) uint4 smask[kWaves][NR_MASK_LAYERS][64];
     {
         const uint4* gm = reinterpret_cast<const uint4*>(SV + nr_sv_mask(nb)) +
-                          (GA ? (size_t)(s >> 5) * NR_MASK_LAYERS * 64 + 32 * h + (s & 31)
-                              : (size_t)blk * NR_MASK_LAYERS * 64 + lane);
+                          (GM == 1 ? (size_t)(s >> 5) * NR_MASK_LAYERS * 64 + 32 * h + (s & 31)
+                                   : (size_t)blk * NR_MASK_LAYERS * 64 + lane);
 #pragma unroll
         for (int l = 0; l < (SO ? 8 : NR_MASK_LAYERS); ++l)   // SO: h1..h8, no hdir
             __builtin_amdgcn_global_load_lds(
@@ -188,7 +192,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
 namespace {
 int bwd_launch(const char* name, bool so, const float* packed_bwd, const float* head,
                const float* out, const float* g_out, const float* save, int64_t n,
-               float* grad_ws, const int32_t* slist, const int32_t* scount, void* stream) {
+               float* grad_ws, const int32_t* slist, const int32_t* scount, void* stream,
+               bool listed_save = false) {
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "%s: n out of range", name);
     if (n == 0) return 0;
     NR_REQUIRE(packed_bwd && head && out && g_out && save && grad_ws, "%s: null pointer", name);
@@ -198,10 +203,12 @@ int bwd_launch(const char* name, bool so, const float* packed_bwd, const float* 
     BwdArgs a{packed_bwd, head, out, g_out, save, (int)n, grad_ws, slist, scount};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
     hipStream_t st = (hipStream_t)stream;
-    if (so && slist) mlp_bwd_kernel<true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
-    else if (so) mlp_bwd_kernel<true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
-    else if (slist) mlp_bwd_kernel<false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
-    else mlp_bwd_kernel<false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+    if (so && slist && listed_save) mlp_bwd_kernel<true, 2><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else if (slist && listed_save) mlp_bwd_kernel<false, 2><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else if (so && slist) mlp_bwd_kernel<true, 1><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else if (so) mlp_bwd_kernel<true, 0><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else if (slist) mlp_bwd_kernel<false, 1><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else mlp_bwd_kernel<false, 0><<<blocks, 64 * kWaves, 0, st>>>(a);
     NR_LAUNCH_CHECK(name);
     return 0;
 }
@@ -240,4 +247,22 @@ NR_API int nr_mlp_bwd_sigma_active(const float* packed_bwd, const float* head, c
     NR_REQUIRE(n == 0 || (samples && count), "nr_mlp_bwd_sigma_active: null sample list");
     return bwd_launch("nr_mlp_bwd_sigma_active", true, packed_bwd, head, out, g_out, save, n,
                       grad_ws, samples, count, stream);
+}
+
+// the deferred save (nr_mlp_fwd_listed): the listed samples' activations saved by position
+NR_API int nr_mlp_bwd_listed(const float* packed_bwd, const float* head, const float* out,
+                             const float* g_out, const float* save, int64_t n, float* grad_ws,
+                             const int32_t* samples, const int32_t* count, void* stream) {
+    NR_REQUIRE(n == 0 || (samples && count), "nr_mlp_bwd_listed: null sample list");
+    return bwd_launch("nr_mlp_bwd_listed", false, packed_bwd, head, out, g_out, save, n, grad_ws,
+                      samples, count, stream, true);
+}
+
+NR_API int nr_mlp_bwd_sigma_listed(const float* packed_bwd, const float* head, const float* out,
+                                   const float* g_out, const float* save, int64_t n,
+                                   float* grad_ws, const int32_t* samples, const int32_t* count,
+                                   void* stream) {
+    NR_REQUIRE(n == 0 || (samples && count), "nr_mlp_bwd_sigma_listed: null sample list");
+    return bwd_launch("nr_mlp_bwd_sigma_listed", true, packed_bwd, head, out, g_out, save, n,
+                      grad_ws, samples, count, stream, true);
 }

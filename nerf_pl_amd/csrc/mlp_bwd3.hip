@@ -163,8 +163,12 @@ struct Bwd3Args {
 // head, dir layer or xyz_encoding_final, so the chain starts at d h8 =
 // W_sigma^T dsigma and the ring streams the transposed weights from layer 8
 // on (the packed buffer from group kL8T, the group indices shifted by kB)
-// GA: over the packed sample list a.slist (the *_active entry points)
-template <bool SO, bool GA>
+// GM (sample-list mode): 0 = every sample; 1 = over the packed sample list
+// a.slist (the *_active entry points): position q < m runs sample slist[q],
+// whose saved activations and masks are gathered; 2 = the same list over a
+// save buffer written by position (nr_mlp_fwd_listed*, the deferred save):
+// masks by position, only g_out / out gathered
+template <bool SO, int GM>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     constexpr int kB = SO ? kL8T : 0;      // first k-group streamed
     constexpr int QE = kQ - kB;            // groups streamed
@@ -179,6 +183,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     // workgroups past its end only zero their stats slots: the weight
     // gradient reads positions < m only
     int m = a.n;
+    constexpr bool GA = GM != 0;
     if constexpr (GA) {
         m = __builtin_amdgcn_readfirstlane(*a.scount);
         if ((int)blockIdx.x * kWaves * 32 >= m) {
@@ -207,7 +212,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         valid[S] = q < m;
         sidx[S] = !valid[S] ? (GA ? 0 : a.n - 1) : (GA ? a.slist[q] : q);
     }
-    if constexpr (!GA) {
+    if constexpr (GM != 1) {
         const uint4* gm = reinterpret_cast<const uint4*>(SV + nr_sv_mask(nb)) +
                           (size_t)blk * NR_MASK_LAYERS * 64 + lane;
 #pragma unroll
@@ -498,7 +503,7 @@ namespace {
 int bwd3_launch(const char* name, bool sigma_only, const void* packed_bwd, const float* head,
                 const float* out, const float* g_out, const float* save, int64_t n,
                 float* grad_ws, void* stream, const int32_t* slist = nullptr,
-                const int32_t* scount = nullptr) {
+                const int32_t* scount = nullptr, bool listed_save = false) {
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "%s: n out of range", name);
     if (n == 0) return 0;
     NR_REQUIRE(packed_bwd && head && out && g_out && save && grad_ws, "%s: null pointer", name);
@@ -511,15 +516,18 @@ int bwd3_launch(const char* name, bool sigma_only, const void* packed_bwd, const
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
     hipStream_t st = (hipStream_t)stream;
 #if NR_BF1     // no sample lists for the bf16 variant
-    if (sigma_only) mlp_bwd3_kernel<true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
-    else mlp_bwd3_kernel<false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+    if (sigma_only) mlp_bwd3_kernel<true, 0><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else mlp_bwd3_kernel<false, 0><<<blocks, 64 * kWaves, 0, st>>>(a);
 #else
-    if (slist) {
-        if (sigma_only) mlp_bwd3_kernel<true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
-        else mlp_bwd3_kernel<false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+    if (slist && listed_save) {
+        if (sigma_only) mlp_bwd3_kernel<true, 2><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_bwd3_kernel<false, 2><<<blocks, 64 * kWaves, 0, st>>>(a);
+    } else if (slist) {
+        if (sigma_only) mlp_bwd3_kernel<true, 1><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_bwd3_kernel<false, 1><<<blocks, 64 * kWaves, 0, st>>>(a);
     } else {
-        if (sigma_only) mlp_bwd3_kernel<true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
-        else mlp_bwd3_kernel<false, false><<<blocks, 64 * kWaves, 0, st>>>(a);
+        if (sigma_only) mlp_bwd3_kernel<true, 0><<<blocks, 64 * kWaves, 0, st>>>(a);
+        else mlp_bwd3_kernel<false, 0><<<blocks, 64 * kWaves, 0, st>>>(a);
     }
 #endif
     NR_LAUNCH_CHECK(name);
@@ -563,5 +571,24 @@ NR_API int NR_X3_NAME(nr_mlp_bwd_sigma_active)(const void* packed_bwd, const flo
     NR_REQUIRE(samples && count, "nr_mlp_bwd_sigma_active: null sample list");
     return bwd3_launch("nr_mlp_bwd_sigma_active", true, packed_bwd, head, out, g_out, save, n,
                        grad_ws, stream, samples, count);
+}
+// the deferred save: the same list over a save buffer nr_mlp_fwd_listed* wrote
+// by position (masks read by position, g_out / out gathered by the list)
+NR_API int NR_X3_NAME(nr_mlp_bwd_listed)(const void* packed_bwd, const float* head,
+                                         const float* out, const float* g_out, const float* save,
+                                         int64_t n, float* grad_ws, const int32_t* samples,
+                                         const int32_t* count, void* stream) {
+    NR_REQUIRE(samples && count, "nr_mlp_bwd_listed: null sample list");
+    return bwd3_launch("nr_mlp_bwd_listed", false, packed_bwd, head, out, g_out, save, n, grad_ws,
+                       stream, samples, count, true);
+}
+NR_API int NR_X3_NAME(nr_mlp_bwd_sigma_listed)(const void* packed_bwd, const float* head,
+                                               const float* out, const float* g_out,
+                                               const float* save, int64_t n, float* grad_ws,
+                                               const int32_t* samples, const int32_t* count,
+                                               void* stream) {
+    NR_REQUIRE(samples && count, "nr_mlp_bwd_sigma_listed: null sample list");
+    return bwd3_launch("nr_mlp_bwd_sigma_listed", true, packed_bwd, head, out, g_out, save, n,
+                       grad_ws, stream, samples, count, true);
 }
 #endif

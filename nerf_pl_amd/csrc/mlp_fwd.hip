@@ -105,18 +105,25 @@ struct FwdArgs {
     int xstride;
     float* out;          // (n, 4) [rgb, sigma] or (n, 1) sigma
     float* save;         // saved activations (training) or nullptr
+    // LIST (nr_mlp_fwd_listed): position q < *scount evaluates sample slist[q],
+    // activations saved by position, no output
+    const int32_t* slist; const int32_t* scount;
 };
 
-template <int MODE, bool SIGMA_ONLY>
+// LIST: the deferred save of a training forward (mlp_fwd3.hip);
+// blk is then a block of positions
+template <int MODE, bool SIGMA_ONLY, bool LIST = false>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     constexpr bool EMB = MODE == FWD_EMB;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
     const int blk = blockIdx.x * kWaves + wave;           // 32-sample block of this wave
+    const int m = LIST ? __builtin_amdgcn_readfirstlane(*a.scount) : a.n;
+    if (LIST && (int)blockIdx.x * kWaves * 32 >= m) return;   // whole workgroup, before the barrier
     const int s_raw = blk * 32 + (lane & 31);
-    const bool valid = s_raw < a.n;
-    const int s = valid ? s_raw : a.n - 1;
+    const bool valid = s_raw < m;
+    const int s = LIST ? a.slist[valid ? s_raw : 0] : (valid ? s_raw : a.n - 1);
     const float* P = a.packed;
     // biases and the sigma/rgb heads come from LDS so their reads never queue
     // behind in-flight weight loads (vmcnt retires in issue order)
@@ -129,7 +136,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     }
     const float* H = Hs;
     const int nb = (int)nr_blocks_pad(a.n);             // segment stride (padded)
-    const bool save = a.save != nullptr && blk < (a.n + 31) / 32;   // whole block, tail lanes included
+    const bool save = a.save != nullptr && blk < (m + 31) / 32;   // whole block, tail lanes included
     float* const SV = a.save;
 
     // ---- point and direction ------------------------------------------------
@@ -231,7 +238,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
                 store_native<8>(B, hseg(7), lane);
                 store_mask<8>(B, mseg(7), lane);
             }
-            if (valid && h == 0)
+            if (valid && h == 0 && !LIST)
                 *reinterpret_cast<f32x4*>(a.out + (size_t)s * 4) = f32x4{0.f, 0.f, 0.f, sigma};
         } else if (valid && h == 0) {
             a.out[s] = sigma;
@@ -273,7 +280,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
             const float zc = head_dot<4>(C, H + NR_H_WRGB + 128 * c, h) + H[NR_H_BRGB + c];
             rgb[c] = 1.f / (1.f + expf(-zc));
         }
-        if (valid && h == 0) {
+        if (valid && h == 0 && !LIST) {
             f32x4 o = {rgb[0], rgb[1], rgb[2], sigma};
             *reinterpret_cast<f32x4*>(a.out + (size_t)s * 4) = o;
         }
@@ -315,6 +322,27 @@ NR_API int nr_mlp_fwd(const float* packed, const float* rays, const float* z, in
         else mlp_fwd_kernel<FWD_RAYS, false><<<blocks, 64 * kWaves, 0, st>>>(a);
     }
     NR_LAUNCH_CHECK("nr_mlp_fwd");
+    return 0;
+}
+
+// the deferred save: the training forward's activations of the samples listed
+// in samples[0 .. *count), saved by position into save (sized for n samples)
+NR_API int nr_mlp_fwd_listed(const float* packed, const float* rays, const float* z, int64_t n,
+                             int samples_per_ray, int sigma_only, float* save,
+                             const int32_t* samples, const int32_t* count, void* stream) {
+    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_fwd_listed: n=%lld out of range", (long long)n);
+    if (n == 0) return 0;
+    NR_REQUIRE(packed && rays && z && save && samples && count && samples_per_ray > 0,
+               "nr_mlp_fwd_listed: null pointer or samples_per_ray");
+    NR_REQUIRE(((uintptr_t)packed & 15) == 0 && ((uintptr_t)save & 15) == 0,
+               "nr_mlp_fwd_listed: packed/save must be 16-byte aligned");
+    FwdArgs a{packed, nullptr, rays, z, nullptr, (int)n, samples_per_ray, 0, nullptr, save, samples,
+              count};
+    const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
+    hipStream_t st = (hipStream_t)stream;
+    if (sigma_only) mlp_fwd_kernel<FWD_RAYS, true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else mlp_fwd_kernel<FWD_RAYS, false, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+    NR_LAUNCH_CHECK("nr_mlp_fwd_listed");
     return 0;
 }
 

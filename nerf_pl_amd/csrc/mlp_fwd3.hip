@@ -192,6 +192,9 @@ struct Fwd3Args {
     const float* pts; const float* rays; const float* z; const float* x;
     int n, spr, xstride;
     float* out; float* save;
+    // LIST (nr_mlp_fwd_listed*): position q < *scount evaluates sample
+    // slist[q]; activations are saved by position, no output is written
+    const int32_t* slist; const int32_t* scount;
 };
 
 // B units of an accumulator input (x3.h Act): the producer's activation
@@ -293,22 +296,32 @@ __device__ __forceinline__ void drain_all(GetU& u) {
     }
 }
 
-template <int MODE, bool SIGMA_ONLY, bool SAVE>
+// LIST: the deferred save of a training forward (nr_mlp_fwd_listed*): the
+// forward ran without saving (the inference kernel, whose layers are these
+// layers bit for bit), and the backward re-evaluates only the samples its
+// sample list names, saving their activations packed by position -- the
+// sigma-only graph's backward lists ~0.1% of a light image's samples and
+// ~20% of the camera rays' (DESIGN.md 11).  blk is then a block of positions.
+template <int MODE, bool SIGMA_ONLY, bool SAVE, bool LIST = false>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     constexpr bool EMB = MODE == FWD_EMB;
     constexpr int QEND = SIGMA_ONLY ? kQSigma : kQAll;
+    static_assert(!LIST || (SAVE && MODE == FWD_RAYS), "a listed run saves, on the ray path");
     __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4;
     const int blk = blockIdx.x * kWaves + wave;
+    const int m = LIST ? __builtin_amdgcn_readfirstlane(*a.scount) : a.n;
+    if (LIST && (int)blockIdx.x * kWaves * 32 >= m) return;   // whole workgroup: before any barrier
     int smp[2];
     bool valid[2];
 #pragma unroll
     for (int S = 0; S < 2; ++S) {
         const int s_raw = blk * 32 + 16 * S + (lane & 15);
-        valid[S] = s_raw < a.n;
-        smp[S] = valid[S] ? s_raw : a.n - 1;
+        valid[S] = s_raw < m;
+        if constexpr (LIST) smp[S] = a.slist[valid[S] ? s_raw : 0];
+        else smp[S] = valid[S] ? s_raw : a.n - 1;
     }
     const char* P = a.packed;
 #if NR_X3_DBG == 8
@@ -461,7 +474,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             p += __shfl_xor(p, 32);
             sigma[S] = p + H[NR_H_BSIG];
         }
-        if (wr) *reinterpret_cast<f32x4*>(a.out + (size_t)sw * 4) = f32x4{0.f, 0.f, 0.f, Sw ? sigma[1] : sigma[0]};
+        if (wr && !LIST)
+            *reinterpret_cast<f32x4*>(a.out + (size_t)sw * 4) = f32x4{0.f, 0.f, 0.f, Sw ? sigma[1] : sigma[0]};
         return;
     } else if constexpr (SIGMA_ONLY) {
         { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, nonext, bi, none, b, f0); }
@@ -508,7 +522,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         float zc[3][2];
 #pragma unroll
         for (int c = 0; c < 3; ++c) head_dot<true>(C, H + NR_H_WRGB + 128 * c, g, zc[c]);
-        if (wr) {
+        if (wr && !LIST) {
             f32x4 o;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -639,6 +653,31 @@ NR_API int NR_X3_NAME(nr_mlp_fwd)(const void* packed, const float* rays, const f
     NR_LAUNCH_CHECK("nr_mlp_fwd_x3");
     return 0;
 }
+
+#if !NR_BF1   // no sample lists for the bf16 variant
+// the deferred save (LIST above): the training forward's activations of the
+// samples listed in samples[0 .. *count) (nr_active_samples), saved by
+// position into save (sized for n samples, as nr_mlp_fwd's); no output
+NR_API int NR_X3_NAME(nr_mlp_fwd_listed)(const void* packed, const float* rays, const float* z,
+                                         int64_t n, int samples_per_ray, int sigma_only,
+                                         float* save, const int32_t* samples,
+                                         const int32_t* count, void* stream) {
+    NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "nr_mlp_fwd_listed: n=%lld out of range", (long long)n);
+    if (n == 0) return 0;
+    NR_REQUIRE(packed && rays && z && save && samples && count && samples_per_ray > 0,
+               "nr_mlp_fwd_listed: null pointer or samples_per_ray");
+    NR_REQUIRE(((uintptr_t)packed & 15) == 0 && ((uintptr_t)save & 15) == 0,
+               "nr_mlp_fwd_listed: packed/save must be 16-byte aligned");
+    Fwd3Args a{reinterpret_cast<const char*>(packed), nullptr, rays, z, nullptr, (int)n,
+               samples_per_ray, 0, nullptr, save, samples, count};
+    const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
+    hipStream_t st = (hipStream_t)stream;
+    if (sigma_only) mlp_fwd3_kernel<FWD_RAYS, true, true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+    else mlp_fwd3_kernel<FWD_RAYS, false, true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
+    NR_LAUNCH_CHECK("nr_mlp_fwd_listed");
+    return 0;
+}
+#endif
 
 NR_API int NR_X3_NAME(nr_mlp_sigma_points)(const void* packed, const float* pts, int64_t n,
                                   float* sigma_out, void* stream) {

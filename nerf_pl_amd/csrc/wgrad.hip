@@ -1277,9 +1277,13 @@ NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
 #endif
 
 namespace {
+// slist / scount: the launch covers positions 0 .. *scount of the buffers; with
+// gather the input operands are gathered from sample slist[q] (the *_active
+// entry points), else they were saved by position (the *_listed ones)
 int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_ws, int64_t n,
                  float* workspace, float* grad_flat, void* stream,
-                 const int32_t* slist = nullptr, const int32_t* scount = nullptr) {
+                 const int32_t* slist = nullptr, const int32_t* scount = nullptr,
+                 bool gather = true) {
     const char* name = sigma_only ? "nr_wgrad_sigma" : "nr_wgrad";
     NR_REQUIRE(n >= 0 && n < (int64_t)1 << 31, "%s: n out of range", name);
     NR_REQUIRE(save && grad_ws && workspace && grad_flat, "%s: null pointer", name);
@@ -1399,18 +1403,18 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
 #if NR_F16
     stats_reduce_kernel<<<NR_STAT_SEGS, kStatT, 0, st>>>(SV + nr_sv_stats(nbp), (int)nbp);
     NR_LAUNCH_CHECK("nr_wgrad_stats");
-    if (slist && !sigma_only) wgrad3_kernel<true, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
-    else if (slist) wgrad3_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    if (slist && gather && !sigma_only) wgrad3_kernel<true, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (slist && gather) wgrad3_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else if (!sigma_only) wgrad3_kernel<false, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else wgrad3_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #elif NR_BF1
     wgrad3_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #else
-    if (x3 && slist && !sigma_only) wgrad3_kernel<true, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
-    else if (x3 && slist) wgrad3_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    if (x3 && slist && gather && !sigma_only) wgrad3_kernel<true, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (x3 && slist && gather) wgrad3_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else if (x3 && !sigma_only) wgrad3_kernel<false, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else if (x3) wgrad3_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
-    else if (slist) wgrad_kernel<true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (slist && gather) wgrad_kernel<true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else wgrad_kernel<false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #endif
     NR_LAUNCH_CHECK("nr_wgrad");
@@ -1444,6 +1448,20 @@ NR_API int nr_wgrad_sigma_active(const float* save, const float* grad_ws, int64_
     NR_REQUIRE(samples && count, "nr_wgrad_sigma_active: null sample list");
     return wgrad_launch(false, true, save, grad_ws, n, workspace, grad_flat, stream, samples, count);
 }
+NR_API int nr_wgrad_listed(const float* save, const float* grad_ws, int64_t n, float* workspace,
+                           float* grad_flat, const int32_t* samples, const int32_t* count,
+                           void* stream) {
+    NR_REQUIRE(samples && count, "nr_wgrad_listed: null sample list");
+    return wgrad_launch(false, false, save, grad_ws, n, workspace, grad_flat, stream, samples, count,
+                        false);
+}
+NR_API int nr_wgrad_sigma_listed(const float* save, const float* grad_ws, int64_t n,
+                                 float* workspace, float* grad_flat, const int32_t* samples,
+                                 const int32_t* count, void* stream) {
+    NR_REQUIRE(samples && count, "nr_wgrad_sigma_listed: null sample list");
+    return wgrad_launch(false, true, save, grad_ws, n, workspace, grad_flat, stream, samples, count,
+                        false);
+}
 #endif
 
 NR_API int NR_X3_NAME(nr_wgrad)(const float* save, const float* grad_ws, int64_t n, float* workspace,
@@ -1474,5 +1492,22 @@ NR_API int NR_X3_NAME(nr_wgrad_sigma_active)(const float* save, const float* gra
                                              void* stream) {
     NR_REQUIRE(samples && count, "nr_wgrad_sigma_active: null sample list");
     return wgrad_launch(true, true, save, grad_ws, n, workspace, grad_flat, stream, samples, count);
+}
+// over the first *count positions of buffers written by position
+// (nr_mlp_fwd_listed* + nr_mlp_bwd*_listed, the deferred save)
+NR_API int NR_X3_NAME(nr_wgrad_listed)(const float* save, const float* grad_ws, int64_t n,
+                                       float* workspace, float* grad_flat, const int32_t* samples,
+                                       const int32_t* count, void* stream) {
+    NR_REQUIRE(samples && count, "nr_wgrad_listed: null sample list");
+    return wgrad_launch(true, false, save, grad_ws, n, workspace, grad_flat, stream, samples, count,
+                        false);
+}
+NR_API int NR_X3_NAME(nr_wgrad_sigma_listed)(const float* save, const float* grad_ws, int64_t n,
+                                             float* workspace, float* grad_flat,
+                                             const int32_t* samples, const int32_t* count,
+                                             void* stream) {
+    NR_REQUIRE(samples && count, "nr_wgrad_sigma_listed: null sample list");
+    return wgrad_launch(true, true, save, grad_ws, n, workspace, grad_flat, stream, samples, count,
+                        false);
 }
 #endif

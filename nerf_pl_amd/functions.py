@@ -45,6 +45,16 @@ ACTIVE_SAMPLES = os.environ.get("NERF_PL_AMD_ACTIVE_SAMPLES", "1") != "0"
 # the arithmetics with *_active entry points (the bf16 variant keeps its
 # sample-major 16x16 bf16 chunks whole: no gather)
 ACTIVE_ARITHS = ("f16x3", "bf16x6", "fp32")
+# Deferred save: a training forward whose backward will list
+# few samples runs without saving activations (the inference kernel), and the
+# backward re-evaluates the listed samples only, saving them by position
+# (nr_mlp_fwd_listed*) -- exact: the recomputed layers are the forward's layers
+# bit for bit.  "sigma" (default): the sigma-only graphs of the shadow path
+# (rendering_shadows.py:167), whose backward lists ~0.1% of a light image's
+# samples and ~20% of the camera rays'; "all": every training forward; "none"
+DEFER_SAVE = os.environ.get("NERF_PL_AMD_DEFER_SAVE", "sigma")
+if DEFER_SAVE not in ("sigma", "all", "none"):
+    raise ValueError(f"NERF_PL_AMD_DEFER_SAVE must be sigma, all or none, got {DEFER_SAVE!r}")
 # bench.py's kernel timer: a list every backward appends its (sample list
 # buffer, index of its length) to, so the rooflines count the samples worked on
 ACTIVE_LOG = None
@@ -72,18 +82,27 @@ class _FusedMLP(torch.autograd.Function):
         # xyz_encoding_final / dir / rgb work), in every arithmetic
         so_train = train and sigma_only and SIGMA_TRAIN_KERNELS and x is None
         kern_sigma_only = sigma_only and (not train or so_train)
+        defer = (train and x is None and ACTIVE_SAMPLES and ops.arith_of(packed_b) in ACTIVE_ARITHS
+                 and (DEFER_SAVE == "all" or (DEFER_SAVE == "sigma" and so_train)))
         out, save = ops.mlp_forward(packed_f, rays=rays, z=z, samples_per_ray=spr, x=x,
-                                    sigma_only=kern_sigma_only, save=train)
+                                    sigma_only=kern_sigma_only, save=train and not defer)
         if train:
-            ctx.save_for_backward(out, save, packed_f, packed_b)
+            if defer:     # the backward recomputes the listed samples' activations
+                ctx.save_for_backward(out, rays, z, packed_f, packed_b)
+                ctx.spr = spr
+            else:
+                ctx.save_for_backward(out, save, packed_f, packed_b)
+            ctx.defer = defer
             ctx.sigma_only = sigma_only
             ctx.so_kernels = so_train
-        if sigma_only and train:
+        if sigma_only and train and out.shape[1] == 4:
             out = out[:, 3:4].contiguous()
         return out
 
     @staticmethod
     def backward(ctx, g_out):
+        if ctx.defer:
+            return _FusedMLP._backward_deferred(ctx, g_out)
         out, save, packed_f, packed_b = ctx.saved_tensors
         n = out.shape[0]
         dev = out.device
@@ -115,15 +134,57 @@ class _FusedMLP(torch.autograd.Function):
         if _DEBUG is not None:
             _DEBUG.update(save=save, grad_ws=grad_ws, g_out=g_out, gflat=gflat, n=n)
             _DEBUG.setdefault("g_outs", []).append(g_out)
-        grads, off = [], 0
-        for name, shp in _SHAPES:
-            k = 1
-            for d in shp:
-                k *= d
-            g = gflat[off:off + k].view(shp)
-            off += k
-            grads.append(None if (ctx.sigma_only and name in _SIGMA_ONLY_UNUSED) else g)
-        return (None,) * 6 + tuple(grads)
+        return (None,) * 6 + _param_grads(gflat, ctx.sigma_only)
+
+    @staticmethod
+    def _backward_deferred(ctx, g_out):
+        """The deferred save's backward: the sample list of g_out, the training
+        forward re-run over the listed samples (activations saved by position),
+        then the data and weight gradients over those positions."""
+        out, rays, z, packed_f, packed_b = ctx.saved_tensors
+        n = z.numel()
+        dev = z.device
+        if g_out.shape[1] == 1:            # a sigma-only graph's d sigma
+            g4 = torch.zeros(n, 4, device=dev)
+            g4[:, 3:4] = g_out
+            g_out = g4
+        g_out = g_out.contiguous()
+        if out.shape[1] != 4:              # the rgb rows only feed the rgb head's backward
+            out = g_out
+        st = stream_of(dev)
+        sl = torch.empty(n + 1 + 2 * ((n + 31) // 32), dtype=torch.int32, device=dev)
+        call("nr_active_samples", g_out.data_ptr(), n, sl.data_ptr(), sl.data_ptr() + 4 * n,
+             sl.data_ptr() + 4 * (n + 1), st)
+        lst = (sl.data_ptr(), sl.data_ptr() + 4 * n)
+        if ACTIVE_LOG is not None:
+            ACTIVE_LOG.append((sl, n))
+        so = ctx.so_kernels
+        save = torch.empty(ops.save_floats(n), device=dev)
+        call(ops.entry("nr_mlp_fwd_listed", packed_f), packed_f.data_ptr(), rays.data_ptr(),
+             z.data_ptr(), n, int(ctx.spr), int(so), save.data_ptr(), *lst, st)
+        grad_ws = torch.empty(ops.n_blocks(n) * ops.GRAD_PER_BLOCK, device=dev)
+        sfx = "_sigma_listed" if so else "_listed"
+        call(ops.entry("nr_mlp_bwd" + sfx, packed_b), packed_b.data_ptr(), ops.head_ptr(packed_f),
+             out.data_ptr(), g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), *lst, st)
+        gflat = torch.empty(packing.N_PARAMS, device=dev)
+        ws = _wgrad_workspace(dev.index, int(st))
+        call(ops.entry("nr_wgrad" + sfx, packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
+             ws.data_ptr(), gflat.data_ptr(), *lst, st)
+        return (None,) * 6 + _param_grads(gflat, ctx.sigma_only)
+
+
+def _param_grads(gflat, sigma_only):
+    """one view of the flat gradient per NeRF parameter (named_parameters
+    order); None for the parameters a sigma-only graph does not reach"""
+    grads, off = [], 0
+    for name, shp in _SHAPES:
+        k = 1
+        for d in shp:
+            k *= d
+        g = gflat[off:off + k].view(shp)
+        off += k
+        grads.append(None if (sigma_only and name in _SIGMA_ONLY_UNUSED) else g)
+    return tuple(grads)
 
 
 def mlp_apply(model, *, rays=None, z=None, spr=0, x=None, sigma_only=False):

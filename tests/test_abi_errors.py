@@ -34,6 +34,15 @@ def _cases():
                   (f"nr_mlp_bwd_sigma{sfx}", [N, N, N, N, N, 5, N, N], NR_EINVAL),
                   (f"nr_wgrad_sigma{sfx}", [N, N, -1, N, N, N], NR_EINVAL),
                   (f"nr_wgrad_sigma{sfx}", [N, N, 5, N, N, N], NR_EINVAL)]
+        if sfx in ("", "_x3", "_h3"):     # deferred save (not the bf16 variant)
+            c += [(f"nr_mlp_fwd_listed{sfx}", [N, N, N, -1, 64, 1, N, N, N, N], NR_EINVAL),
+                  (f"nr_mlp_fwd_listed{sfx}", [N, N, N, 0, 64, 1, N, N, N, N], 0),
+                  (f"nr_mlp_fwd_listed{sfx}", [N, N, N, 5, 64, 1, N, N, N, N], NR_EINVAL)]
+            for so in ("", "_sigma"):
+                c += [(f"nr_mlp_bwd{so}_listed{sfx}", [N, N, N, N, N, -1, N, N, N, N], NR_EINVAL),
+                      (f"nr_mlp_bwd{so}_listed{sfx}", [N, N, N, N, N, 5, N, N, N, N], NR_EINVAL),
+                      (f"nr_wgrad{so}_listed{sfx}", [N, N, -1, N, N, N, N, N], NR_EINVAL),
+                      (f"nr_wgrad{so}_listed{sfx}", [N, N, 5, N, N, N, N, N], NR_EINVAL)]
         if sfx in ("", "_x3", "_h3"):     # zero-gradient sample lists (not the bf16 variant)
             for so in ("", "_sigma"):
                 c += [(f"nr_mlp_bwd{so}_active{sfx}", [N, N, N, N, N, -1, N, N, N, N], NR_EINVAL),

@@ -126,6 +126,43 @@ def test_active_backward_matches_every_sample(math, case, sigma_only, monkeypatc
         assert dev <= 2e-6, f"{math} {case} {k}: {dev:.3g}"
 
 
+@pytest.mark.parametrize("math", ["f16x3", "fp32"])
+def test_deferred_save_full_graph(math, monkeypatch):
+    """NERF_PL_AMD_DEFER_SAVE=all on the full graph (render_rays' training
+    step): the forward as inference, the listed samples' activations
+    re-evaluated in the backward and saved by position -- the same loss and
+    the same gradients bit for bit as the sample-list backward over a
+    forward-time save"""
+    from nerf_pl_amd import Embedding, NeRF, ReplayRNG, functions, ops, render_rays
+    from nerf_pl_amd.rays import blender_rays
+    monkeypatch.setattr(ops, "MATH", math)
+    n, S, I = 512, 64, 64
+    rays = blender_rays(32, 1, near=2.0, far=6.0)[:n].contiguous().to(DEV)
+    g = torch.Generator().manual_seed(19)
+    draws = [torch.rand(n, S, generator=g), torch.randn(n, S, generator=g),
+             torch.rand(n, I, generator=g), torch.rand(n, I, generator=g),
+             torch.randn(n, S + I, generator=g)]
+    tgt = torch.rand(n, 3, generator=g).to(DEV)
+    res = []
+    for defer in ("all", "none"):
+        monkeypatch.setattr(functions, "DEFER_SAVE", defer)
+        models = []
+        for s in (13, 14):
+            m = NeRF()
+            m.load_state_dict(O.make_params(s, sigma_bias=0.2))
+            models.append(m.to(DEV))
+        out = render_rays(models, [Embedding(3, 10), Embedding(3, 4)], rays, S, False, 1.0, 1.0, I,
+                          32768, False, rng=ReplayRNG([d.clone() for d in draws]))
+        loss = ((out["rgb_coarse"] - tgt) ** 2).mean() + ((out["rgb_fine"] - tgt) ** 2).mean()
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((loss.item(), [[p.grad.detach().cpu() for p in m.parameters()] for m in models]))
+    assert res[0][0] == res[1][0]
+    for ga, gb in zip(res[0][1], res[1][1]):
+        for a, b in zip(ga, gb):
+            assert torch.equal(a, b)
+
+
 def test_active_backward_in_render_rays(monkeypatch):
     """the training step of render_rays (both models, coarse + fine) with and
     without the sample list: same loss, same gradients (1e-6 normwise)"""

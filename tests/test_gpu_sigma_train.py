@@ -17,12 +17,13 @@ DEV = torch.device("cuda", 0)
 S, I = 32, 32
 
 
-def _step(math, so_kernels, monkeypatch, n=700, seed=3):
+def _step(math, so_kernels, monkeypatch, n=700, seed=3, defer="none"):
     from nerf_pl_amd import Embedding, NeRF, ReplayRNG, functions, ops
     from nerf_pl_amd import rendering_shadows as RS
     from nerf_pl_amd.rays import blender_rays
     monkeypatch.setattr(ops, "MATH", math)
     monkeypatch.setattr(functions, "SIGMA_TRAIN_KERNELS", so_kernels)
+    monkeypatch.setattr(functions, "DEFER_SAVE", defer)
     models = []
     for s in (41, 42):
         m = NeRF()
@@ -46,9 +47,13 @@ def _step(math, so_kernels, monkeypatch, n=700, seed=3):
               for name, p in m.named_parameters()] for m in models])
 
 
-@pytest.mark.parametrize("math", ["f16x3", "bf16x6", "bf16", "fp32"])
-def test_sigma_only_training_kernels_match_full_kernels(math, monkeypatch):
-    out_a, grads_a = _step(math, True, monkeypatch)
+@pytest.mark.parametrize("math,defer", [("f16x3", "none"), ("bf16x6", "none"), ("bf16", "none"),
+                                        ("fp32", "none"), ("f16x3", "sigma"), ("bf16x6", "sigma"),
+                                        ("fp32", "sigma")])
+def test_sigma_only_training_kernels_match_full_kernels(math, defer, monkeypatch):
+    """defer = "sigma": the deferred save -- the forward as
+    inference, the listed samples re-evaluated in the backward"""
+    out_a, grads_a = _step(math, True, monkeypatch, defer=defer)
     out_b, grads_b = _step(math, False, monkeypatch)
     for k in out_b:
         assert torch.equal(out_a[k], out_b[k]), k
@@ -63,4 +68,21 @@ def test_sigma_only_training_kernels_match_full_kernels(math, monkeypatch):
             exact += int(torch.equal(a, b))
             dev = ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
             assert dev <= 1e-6, f"{math} {name}: {dev:.3g}"
-    print(f"{math}: {exact} of 36 gradient tensors bit-identical")
+    print(f"{math} defer={defer}: {exact} of 36 gradient tensors bit-identical")
+
+
+@pytest.mark.parametrize("math", ["f16x3", "bf16x6", "fp32"])
+def test_deferred_save_equals_forward_time_save(math, monkeypatch):
+    """The deferred save re-runs the same layers over the listed samples and
+    feeds the backward the same positions in the same order as the sample-list
+    backward over a forward-time save: every output and every gradient
+    bit-identical."""
+    out_a, grads_a = _step(math, True, monkeypatch, defer="sigma")
+    out_b, grads_b = _step(math, True, monkeypatch, defer="none")
+    for k in out_b:
+        assert torch.equal(out_a[k], out_b[k]), k
+    for ga, gb in zip(grads_a, grads_b):
+        for (name, a), (_, b) in zip(ga, gb):
+            assert (a is None) == (b is None), name
+            if a is not None:
+                assert torch.equal(a, b), f"{math} {name}"
