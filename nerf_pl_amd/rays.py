@@ -149,16 +149,21 @@ class RaySampler:
     """Shuffled training batches generated on the device -- replaces the
     reference's ray buffer + ``DataLoader(shuffle=True, batch_size=B)``
     (train.py:89-94): each epoch is a random permutation of all pixels of all
-    poses (torch.randperm on the device), each batch is produced by one
-    ``nr_gen_rays`` launch that also gathers the target colours.
+    poses, each batch is produced by one ``nr_gen_rays`` launch that also
+    gathers the target colours.
 
     Data-parallel runs partition every epoch like the ``DistributedSampler``
-    that Lightning's DDP backend installs (train.py:175): the same
-    permutation on every rank (generator seeded ``seed + epoch``, identical
-    across ranks), padded with its head to a multiple of ``world``, and rank r
-    takes ``perm[r::world]`` -- the ranks' batches are disjoint and together
-    cover the epoch.  An epoch ends when the rank's shard cannot fill another
-    batch (the remainder is dropped)."""
+    that Lightning's DDP backend installs (train.py:175), and with
+    its very permutation: ``torch.randperm`` of the epoch on a CPU generator
+    seeded ``seed + epoch`` (identical on every rank), padded with its head to a
+    multiple of ``world``, rank r taking ``perm[r::world]`` -- the ranks'
+    batches are disjoint and together cover the epoch.  An epoch ends when the
+    rank's shard cannot fill another batch (the remainder is dropped).  The
+    permutation is drawn on the host by a worker thread one epoch ahead and
+    only the rank's shard is copied to the device: a device-side randperm of a
+    64M-pixel pool (cfg4) costs every rank a 64M-key radix sort per epoch, and
+    with several ranks sharing one GPU (the one-GPU rehearsal of the 8-GPU
+    run) four concurrent sorts did not finish in 100 s."""
 
     def __init__(self, c2w, H, W, focal, near, far, rgb_pool=None, ndc=False, seed=0, rank=0,
                  world=1):
@@ -171,15 +176,29 @@ class RaySampler:
         self.seed, self.rank, self.world = seed, rank, world
         self.device = c2w.device
         self.epoch, self.shard, self.pos = -1, None, 0
+        self._pool = None
+        self._ahead = None      # (epoch, future of its host shard)
 
-    def _new_epoch(self):
-        self.epoch += 1
-        gen = torch.Generator(device=self.device).manual_seed(self.seed + self.epoch)
-        perm = torch.randperm(self.total, device=self.device, generator=gen)
+    def _host_shard(self, epoch):
+        gen = torch.Generator().manual_seed(self.seed + epoch)
+        perm = torch.randperm(self.total, generator=gen)
         pad = (-self.total) % self.world          # DistributedSampler(drop_last=False)
         if pad:
             perm = torch.cat([perm, perm[:pad]])
-        self.shard = perm[self.rank::self.world]
+        shard = perm[self.rank::self.world].contiguous()
+        return shard.pin_memory() if self.device.type == "cuda" else shard
+
+    def _new_epoch(self):
+        import concurrent.futures
+        self.epoch += 1
+        if self._pool is None:
+            self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)
+        if self._ahead is not None and self._ahead[0] == self.epoch:
+            host = self._ahead[1].result()
+        else:
+            host = self._host_shard(self.epoch)
+        self._ahead = (self.epoch + 1, self._pool.submit(self._host_shard, self.epoch + 1))
+        self.shard = host.to(self.device, non_blocking=True)
         self.pos = 0
 
     def next_indices(self, batch: int):
