@@ -691,15 +691,17 @@ __device__ __forceinline__ void store_row(const f32x4& v, int F, int S, float* _
 #endif
 }
 
-// NR_ROW_PAIR (A/B knob for the row stores of the full graph's forward):
-// 0 = each 64-B half of a sample's 128-B row line stored as soon as its tile is
-// split (two units apart); 1 = both halves stored back to back; 2 = whole
-// lines: the odd tile's values rotated by 8 lanes within each 16-lane row
-// (DPP row_ror:8 with bank masks, no other VALU), so that one store writes 8
-// samples x 128 B -- full lines instead of the partial 64-B segments that
-// made the forward write 1.30x its bytes (round-3 PMC)
+// NR_ROW_PAIR (the row stores of the full graph's forward): 0 = each 64-B
+// half of a sample's 128-B row line stored as soon as its tile is split (two
+// units apart; round 3); 1 = both halves stored back to back; 2 (shipped) =
+// whole lines: the odd tile's values rotated by 8 lanes within each 16-lane
+// row (DPP row_ror:8 with bank masks), so that one store writes 8 samples x
+// 128 B.  Measured (profiles/r04/ab_rowpair, abalt_pair2): the fine forward's
+// WRITE_SIZE 10.63 -> 8.33 GB (1.30x -> 1.02x its 8.18 GB of activations),
+// its time unchanged, the data gradient that follows it 1.54 -> 1.45 ms and
+// the cfg2 step +1.5% (three alternating rounds on one box)
 #ifndef NR_ROW_PAIR
-#define NR_ROW_PAIR 0
+#define NR_ROW_PAIR 2
 #endif
 constexpr bool kRowPair = NR_ROW_PAIR != 0 && !NR_BF1;
 
