@@ -43,6 +43,13 @@ constexpr bool kFuse = NR_F16 || NR_BF1;
 // bit i: pair i of wgrad_launch's kFused (f16x3 6: no spills, measured slower)
 #define NR_WGRAD_FUSE_MASK 7
 #endif
+// the same for the gathering kernels (the *_active entry points): the fused
+// PE pair (bit 0) leaves wgrad3_kernel<true, ROWS> 33 spilled VGPRs (8
+// without it), and unfused its fine-pass launch runs 1.97 -> 1.83 ms
+// (three alternating same-box rounds, profiles/r04/abalt_fuse6)
+#ifndef NR_WGRAD_FUSE_MASK_GA
+#define NR_WGRAD_FUSE_MASK_GA 6
+#endif
 
 // flat parameter offsets, NeRF.named_parameters() order (packing.py param_offsets)
 struct POff {
@@ -1118,8 +1125,10 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
         switch (__builtin_amdgcn_readfirstlane(T.id)) {
 #if NR_WGRAD_FUSE_MASK & 1
             case 5:    // DZ(4) x [H(3) | PE]: xyz_encoding_5 (skip layer)
-                wgrad3_body<GA, ROWS, SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_PE, 64, 0, NR_WG_PE_WM, 8 / NR_WG_PE_WM>(
-                    a, T, b0, b1, lds, slab, xslab); break;
+                if constexpr (!GA || (NR_WGRAD_FUSE_MASK_GA & 1))
+                    wgrad3_body<GA, ROWS, SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_PE, 64, 0, NR_WG_PE_WM,
+                                8 / NR_WG_PE_WM>(a, T, b0, b1, lds, slab, xslab);
+                break;
 #endif
 #if NR_WGRAD_FUSE_MASK & 2
             case 9:    // [DZ(8) | head] x H(7): xyz_encoding_final and sigma
@@ -1371,8 +1380,11 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     bool absorbed[kTasks];
     for (int t = 0; t < kTasks; ++t) { partner[t] = -1; absorbed[t] = false; }
     if (kFuse && x3 && fuse_on && (tmask_env == -1)) {
+        // the gathering kernel (a list, gathered inputs) has its own pair set
+        const int fmask = (slist && gather && !NR_BF1) ? (NR_WGRAD_FUSE_MASK & NR_WGRAD_FUSE_MASK_GA)
+                                                      : NR_WGRAD_FUSE_MASK;
         for (int i = 0; i < 3; ++i) {
-            if (!((NR_WGRAD_FUSE_MASK >> i) & 1)) continue;
+            if (!((fmask >> i) & 1)) continue;
             const auto& pr = kFused[i];
             if (!((tmask >> pr[0]) & 1) || !((tmask >> pr[1]) & 1)) continue;   // both must run
             gt[pr[1]] = gt[pr[0]] = std::max<int64_t>(1, std::min<int64_t>(
