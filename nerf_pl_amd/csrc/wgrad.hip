@@ -24,6 +24,13 @@ constexpr int kTasks = 14;
 #define NR_WGRAD_TARGET_WG 760
 #endif
 constexpr int kTargetWG = NR_WGRAD_TARGET_WG;   // ~3 rounds of one workgroup per CU (short tail)
+// the gathering kernels (a sample list, gathered inputs): 1024 measured 1.5%
+// faster than 760 at cfg2's fine pass (three alternating rounds, profiles/r04/abalt_tw)
+#ifndef NR_WGRAD_TARGET_WG_GA
+#define NR_WGRAD_TARGET_WG_GA 1024
+#endif
+constexpr int kTargetWGMax = NR_WGRAD_TARGET_WG > NR_WGRAD_TARGET_WG_GA ? NR_WGRAD_TARGET_WG
+                                                                        : NR_WGRAD_TARGET_WG_GA;
 constexpr int kThreads = 512;    // 8 waves: two per SIMD, so one wave's staging and
                                  // barrier time overlaps its partner's MFMAs
 constexpr int kCol = 36;         // LDS column stride (floats): [column][32 samples + 4 pad]
@@ -1281,7 +1288,7 @@ __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
 NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
     (void)n;
     // upper bound of sum_t G_t * (M_t N_t + M_t) for the task list below
-    return (int64_t)(3 * kTargetWG + kTasks) * (256 * 256 + 256) * sizeof(float);
+    return (int64_t)(3 * kTargetWGMax + kTasks) * (256 * 256 + 256) * sizeof(float);
 }
 #endif
 
@@ -1357,6 +1364,7 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     // computed (written as 0; the autograd leaves them None)
     const long long tmask = sigma_only ? (tmask_env & ~((1LL << 9) | (1LL << 10) | (1LL << 11) | (1LL << 13)))
                                        : tmask_env;
+    const int64_t target_wg = (slist && gather) ? NR_WGRAD_TARGET_WG_GA : kTargetWG;
     int64_t gt[kTasks];
     int pos[kTasks];
     for (int k = 0; k < kTasks; ++k) {
@@ -1364,7 +1372,7 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
         // the 4-row head tasks' per-block time is mostly fixed cost, not
         // bytes: always split finer, so they fill the tail of the last round
         const int split = cost[t] >= heavy && tasks[t].a.kind != SEG_HEAD ? 1 : 3;
-        int64_t g = split * ((kTargetWG * cost[t] + tot - 1) / tot);
+        int64_t g = split * ((target_wg * cost[t] + tot - 1) / tot);
         gt[t] = std::max<int64_t>(1, std::min<int64_t>(g, nb));
         if (!((tmask >> t) & 1)) gt[t] = 0;
         pos[t] = k;
@@ -1388,7 +1396,7 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
             const auto& pr = kFused[i];
             if (!((tmask >> pr[0]) & 1) || !((tmask >> pr[1]) & 1)) continue;   // both must run
             gt[pr[1]] = gt[pr[0]] = std::max<int64_t>(1, std::min<int64_t>(
-                (kTargetWG * (cost[pr[0]] + cost[pr[1]]) + tot - 1) / tot, nb));
+                (target_wg * (cost[pr[0]] + cost[pr[1]]) + tot - 1) / tot, nb));
             partner[pr[0]] = pr[1];
             absorbed[pr[1]] = true;
         }
