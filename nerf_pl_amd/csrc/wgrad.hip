@@ -29,7 +29,7 @@ constexpr int kTargetWG = NR_WGRAD_TARGET_WG;   // ~3 rounds of one workgroup pe
 #ifndef NR_WGRAD_TARGET_WG_GA
 #define NR_WGRAD_TARGET_WG_GA 1024
 #endif
-constexpr int kTargetWGMax = NR_WGRAD_TARGET_WG > NR_WGRAD_TARGET_WG_GA ? NR_WGRAD_TARGET_WG
+[[maybe_unused]] constexpr int kTargetWGMax = NR_WGRAD_TARGET_WG > NR_WGRAD_TARGET_WG_GA ? NR_WGRAD_TARGET_WG
                                                                         : NR_WGRAD_TARGET_WG_GA;
 constexpr int kThreads = 512;    // 8 waves: two per SIMD, so one wave's staging and
                                  // barrier time overlaps its partner's MFMAs
