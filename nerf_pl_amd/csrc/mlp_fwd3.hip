@@ -25,8 +25,16 @@ using namespace x3;
 constexpr int kHeadBytes = NR_H_SIZE * 4;
 constexpr int kHeadDma = (kHeadBytes + 1023) / 1024;   // 1 KiB LDS-DMA instructions for the head
 constexpr int kHeadLds = kHeadDma * 1024;
+// NR_PE_REGS: keep the encodings in registers for layer 5 and the dir layer
+// (224 VGPRs, no spill) instead of parking them in LDS (48 KiB).  Measured
+// (profiles/r04/abalt_peregs, three alternating rounds): fine forward 2.81 ->
+// 2.73 ms; the 48 KiB freed for a 4-super-slot ring (NR_X3_SSLOTS=4 on this
+// object) bought nothing -- ring depth is not what the hand-overs wait for
+#ifndef NR_PE_REGS
+#define NR_PE_REGS 1
+#endif
 constexpr int kPeQ = 12;                          // float4 per lane: xyz PE slots (8), dir PE (4)
-constexpr int kPeBytes = kWaves * kPeQ * 64 * 16;  // each wave's encodings, parked for layer 5 / dir
+constexpr int kPeBytes = NR_PE_REGS ? 0 : kWaves * kPeQ * 64 * 16;  // each wave's encodings, parked for layer 5 / dir
 constexpr int kLdsBytes = kRingBytes + kHeadLds + kPeBytes;
 
 // ---- the k-group sequence (packing.py FWD3_LAYERS) --------------------------
@@ -366,7 +374,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 
     // PE slots of both sample tiles (and the direction PE): computed once,
     // parked in LDS for layer 5 and the dir layer
-    f32x4* pe_lds = reinterpret_cast<f32x4*>(smem + kRingBytes + kHeadLds) + wave * kPeQ * 64 + lane;
+    [[maybe_unused]] f32x4* pe_lds =
+        reinterpret_cast<f32x4*>(smem + kRingBytes + kHeadLds) + wave * kPeQ * 64 + lane;
 #pragma unroll
     for (int S = 0; S < 2; ++S) {
         if constexpr (MODE == FWD_PTS) {
@@ -378,6 +387,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             if constexpr (!SIGMA_ONLY) dir_encode(dg[S], in[S][3], in[S][4], in[S][5], g);
         }
     }
+#if !NR_PE_REGS
 #pragma unroll
     for (int q = 0; q < 8; ++q)
         pe_lds[q * 64] = f32x4{pe[q >> 2][4 * (q & 3)], pe[q >> 2][4 * (q & 3) + 1],
@@ -389,6 +399,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
             pe_lds[(9 + 2 * S) * 64] = f32x4{dg[S][4], dg[S][5], dg[S][6], dg[S][7]};
         }
     }
+#endif
 #if NR_X3_DBG == 8
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -430,12 +441,19 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     { auto bi = bias(NR_H_BIAS(3)); segment<FwdTab, kL3, 8, 2, QEND, true>(dma, lane, A, u2, u3, bi, none, b, f0); }
     NR_STAMP(4);
     float pe5[2][16];
+#if NR_PE_REGS
+#pragma unroll
+    for (int S = 0; S < 2; ++S)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) pe5[S][i] = pe[S][i];
+#else
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const f32x4 v = pe_lds[q * 64];
 #pragma unroll
         for (int e = 0; e < 4; ++e) pe5[q >> 2][4 * (q & 3) + e] = v[e];
     }
+#endif
     PeU<16> pe5u{pe5};
     { auto bi = bias(NR_H_BIAS(4)); segment<FwdTab, kL4, 8, 2, QEND, true>(dma, lane, B, u3, pe5u, bi, none, b, f0); }
     NR_STAMP(5);
@@ -490,6 +508,12 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         NR_STAMP(10);
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
         float dpe[2][8];
+#if NR_PE_REGS
+#pragma unroll
+        for (int S = 0; S < 2; ++S)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dpe[S][i] = dg[S][i];
+#else
 #pragma unroll
         for (int S = 0; S < 2; ++S)
 #pragma unroll
@@ -498,6 +522,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) dpe[S][4 * h + e] = v[e];
             }
+#endif
         PeU<8> dpeu{dpe};
         // xyz_encoding_final: no activation (nerf.py:116)
         AccU<false, SAVE, false, false> uf{A, SV + nr_sv_feat(nb) + (size_t)blk * NR_SEGF(256),
