@@ -31,7 +31,7 @@ constexpr int kHeadLds = kHeadDma * 1024;
 // 2.73 ms; the 48 KiB freed for a 4-super-slot ring (NR_X3_SSLOTS=4 on this
 // object) bought nothing -- ring depth is not what the hand-overs wait for
 #ifndef NR_PE_REGS
-#define NR_PE_REGS 1
+#define NR_PE_REGS (NR_F16 || NR_BF1)   // bf16x6's three pieces leave no room (18-30 spills)
 #endif
 constexpr int kPeQ = 12;                          // float4 per lane: xyz PE slots (8), dir PE (4)
 constexpr int kPeBytes = NR_PE_REGS ? 0 : kWaves * kPeQ * 64 * 16;  // each wave's encodings, parked for layer 5 / dir
