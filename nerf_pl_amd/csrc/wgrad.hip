@@ -1364,7 +1364,10 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     // computed (written as 0; the autograd leaves them None)
     const long long tmask = sigma_only ? (tmask_env & ~((1LL << 9) | (1LL << 10) | (1LL << 11) | (1LL << 13)))
                                        : tmask_env;
-    const int64_t target_wg = (slist && gather) ? NR_WGRAD_TARGET_WG_GA : kTargetWG;
+    // every launch over a sample list -- gathering (*_active) or over buffers
+    // saved by position (*_listed, the deferred save) -- uses the same split-K
+    // partition, so the two give bit-identical sums
+    const int64_t target_wg = slist ? NR_WGRAD_TARGET_WG_GA : kTargetWG;
     int64_t gt[kTasks];
     int pos[kTasks];
     for (int k = 0; k < kTasks; ++k) {
@@ -1388,9 +1391,9 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     bool absorbed[kTasks];
     for (int t = 0; t < kTasks; ++t) { partner[t] = -1; absorbed[t] = false; }
     if (kFuse && x3 && fuse_on && (tmask_env == -1)) {
-        // the gathering kernel (a list, gathered inputs) has its own pair set
-        const int fmask = (slist && gather && !NR_BF1) ? (NR_WGRAD_FUSE_MASK & NR_WGRAD_FUSE_MASK_GA)
-                                                      : NR_WGRAD_FUSE_MASK;
+        // launches over a sample list have their own pair set (see target_wg)
+        const int fmask = (slist && !NR_BF1) ? (NR_WGRAD_FUSE_MASK & NR_WGRAD_FUSE_MASK_GA)
+                                             : NR_WGRAD_FUSE_MASK;
         for (int i = 0; i < 3; ++i) {
             if (!((fmask >> i) & 1)) continue;
             const auto& pr = kFused[i];
