@@ -18,10 +18,16 @@ reference by tests/golden) with the reference's random draws replayed:
   truth (the oracle evaluated in float64; near/far 1/200 and the 2^9
   positional-encoding frequency make the step ill-conditioned), so two
   fp32-accurate evaluations can sit up to ~sqrt(2) floor apart: each tensor
-  must be within max(1e-4, sqrt(2) floor) of the fp32 oracle, or at least as
-  close to the float64 truth as the reference's fp32 is (max(1e-4, floor)).
-  Measured on the first run: the exact-fp32 sigma head sat 1.5e-4 from the
-  fp32 oracle but 6.9e-5 from float64, where the oracle's fp32 sits ~9e-5.
+  must be within max(1e-4, sqrt(2) k floor) of the fp32 oracle, or at least as
+  close to the float64 truth as k times the reference's fp32 (max(1e-4,
+  k floor)), k = the arithmetic's per-product error in fp32 roundings: 1 for
+  exact fp32, 12 for f16x3 (3 x 2^-22 against 2^-24, DESIGN.md 3: under the
+  cancellation of the sigma head's sum over samples -- the 1e10 last-sample
+  delta makes d sigma span many binades -- its 22-bit operands show).
+  Measured: the exact-fp32 sigma head 1.5e-4 from the fp32 oracle but 6.9e-5
+  from float64 (the oracle's fp32 ~9e-5 from it) on one batch; on another
+  the f16x3 sigma head 1.5e-3 from float64 where the reference's fp32 sits
+  3.4e-4 from it (4.4 of its 12).
 """
 import math
 
@@ -36,6 +42,8 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 IMG, POSES, S, I, B = 800, 100, 64, 128, 4096
 RANK, WORLD = 5, 8
+# per-product error of the MLP arithmetic in fp32 roundings
+K_ULPS = {"fp32": 1, "f16x3": 12}
 
 
 def _batch():
@@ -177,13 +185,13 @@ def test_cfg4_training_step_gradients_match_oracle(math_, monkeypatch):
             exp, e64 = p[name].grad.double(), q[name].grad
             got = w.grad.detach().cpu().double()
             scale, s64 = exp.norm() + 1e-30, e64.norm() + 1e-30
-            floor = ((exp - e64).norm() / s64).item()
+            floor = K_ULPS[math_] * ((exp - e64).norm() / s64).item()
             bound = max(1e-4, math.sqrt(2) * floor)
             dev = ((got - exp).norm() / scale).item()
             dev64 = ((got - e64).norm() / s64).item()
             ok = dev <= bound or dev64 <= max(1e-4, floor)
             worst = max(worst, min(dev / bound, dev64 / max(1e-4, floor)))
             assert ok, (f"{math_} {name}: {dev:.3g} from the fp32 oracle (bound {bound:.3g}), "
-                        f"{dev64:.3g} from float64 (reference fp32: {floor:.3g})")
+                        f"{dev64:.3g} from float64 (reference fp32 x k: {floor:.3g})")
     assert math.isfinite(worst)
     print(f"cfg4 {math_} gradients: worst deviation {worst:.2f} of its bound")
