@@ -14,20 +14,18 @@ reference by tests/golden) with the reference's random draws replayed:
   (tests/screening.py);
 * the training step's parameter gradients (MSE coarse + fine against the
   batch's target colours, train.py:107) on a 1,024-ray share of the batch.
-  The reference's own fp32 gradient sits a distance `floor` from the float64
-  truth (the oracle evaluated in float64; near/far 1/200 and the 2^9
-  positional-encoding frequency make the step ill-conditioned), so two
-  fp32-accurate evaluations can sit up to ~sqrt(2) floor apart: each tensor
-  must be within max(1e-4, sqrt(2) k floor) of the fp32 oracle, or at least as
-  close to the float64 truth as k times the reference's fp32 (max(1e-4,
-  k floor)), k = the arithmetic's per-product error in fp32 roundings: 1 for
-  exact fp32, 12 for f16x3 (3 x 2^-22 against 2^-24, DESIGN.md 3: under the
-  cancellation of the sigma head's sum over samples -- the 1e10 last-sample
-  delta makes d sigma span many binades -- its 22-bit operands show).
-  Measured: the exact-fp32 sigma head 1.5e-4 from the fp32 oracle but 6.9e-5
-  from float64 (the oracle's fp32 ~9e-5 from it) on one batch; on another
-  the f16x3 sigma head 1.5e-3 from float64 where the reference's fp32 sits
-  3.4e-4 from it (4.4 of its 12).
+  This step is ill-conditioned in fp32 (near/far 1/200: positions up to ~200
+  units out meet the 2^9 positional-encoding frequency): moving every initial
+  weight by one fp32 ulp moves the sigma head's gradient by 4-6e-4 of its norm
+  in the oracle itself, as far as the oracle's fp32 sits from float64
+  (measured on CPU for this batch).  `floor` = the largest of those distances
+  (the oracle's fp32 from float64, and two one-ulp-perturbed fp32 oracles from
+  the unperturbed one); two fp32-accurate evaluations whose activations differ
+  by a few ulps (our GEMM order vs the reference's BLAS) sit a few floors
+  apart, so each tensor must be within max(1e-4, 2 sqrt(2) floor) of the fp32
+  oracle.  First runs: the exact-fp32 sigma head 1.5e-4 from the fp32 oracle
+  (floor ~1e-4) on one batch; 1.1e-3 (f16x3: 1.2e-3) on the next, where the
+  floor is ~6e-4.
 """
 import math
 
@@ -42,8 +40,6 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 IMG, POSES, S, I, B = 800, 100, 64, 128, 4096
 RANK, WORLD = 5, 8
-# per-product error of the MLP arithmetic in fp32 roundings
-K_ULPS = {"fp32": 1, "f16x3": 12}
 
 
 def _batch():
@@ -69,9 +65,18 @@ def _draws(n, seed=17):
             torch.randn(n, S + I, generator=g)]
 
 
-def _params(dt=torch.float32, grad=False):
-    return [{k: v.to(dt).requires_grad_(grad) for k, v in O.make_params(s, sigma_bias=0.5).items()}
-            for s in (31, 32)]
+def _params(dt=torch.float32, grad=False, ulp_seed=None):
+    """the seeded NeRF pair; ulp_seed: every weight moved by one fp32 ulp up or down"""
+    out = []
+    for s in (31, 32):
+        p = {k: v.to(dt) for k, v in O.make_params(s, sigma_bias=0.5).items()}
+        if ulp_seed is not None:
+            g = torch.Generator().manual_seed(ulp_seed + s)
+            for k in p:
+                sgn = torch.randint(0, 2, p[k].shape, generator=g).to(dt) * 2 - 1
+                p[k] = p[k] * (1 + sgn * 2.0 ** -23)
+        out.append({k: v.requires_grad_(grad) for k, v in p.items()})
+    return out
 
 
 def _models():
@@ -166,32 +171,35 @@ def test_cfg4_training_step_gradients_match_oracle(math_, monkeypatch):
     cap = {}
     res = _ours(models, rays, draws, cap)
     p32, p64 = _params(grad=True), _params(torch.float64, grad=True)
+    pu = [_params(grad=True, ulp_seed=u) for u in (1, 2)]
     c32, c64 = {}, {}
     ref = O.render_rays(p32, rays, S, False, 1.0, 1.0, I, 32768, False, rng=O.ReplayRNG(draws),
                         capture=c32)
     ref64 = O.render_rays(p64, rays.double(), S, False, 1.0, 1.0, I, 32768, False,
                           rng=O.ReplayRNG([d.double() for d in draws]), capture=c64)
+    refu = [O.render_rays(p, rays, S, False, 1.0, 1.0, I, 32768, False, rng=O.ReplayRNG(draws))
+            for p in pu]
     bad = _screen(cap, c32, draws)
     z32, z64 = c32["z_fine"].detach().double(), c64["z_fine"].detach()
     bad |= ((z32 - z64).abs().max(1).values > 1e-4 * z64.abs().max(1).values.clamp(min=1)).numpy()
     assert bad.mean() <= 0.02, f"{bad.sum()} rays screened"
     keep = torch.from_numpy(~bad)
     _loss(res, rgbs, keep).backward()
-    _loss(ref, rgbs, keep).backward()
-    _loss(ref64, rgbs, keep).backward()
+    for out in [ref, ref64] + refu:
+        _loss(out, rgbs, keep).backward()
     worst = 0.0
-    for m, p, q in zip(models, p32, p64):
+    for mi, m in enumerate(models):
         for name, w in m.named_parameters():
-            exp, e64 = p[name].grad.double(), q[name].grad
+            exp, e64 = p32[mi][name].grad.double(), p64[mi][name].grad
+            eu = [p[mi][name].grad.double() for p in pu]
             got = w.grad.detach().cpu().double()
-            scale, s64 = exp.norm() + 1e-30, e64.norm() + 1e-30
-            floor = K_ULPS[math_] * ((exp - e64).norm() / s64).item()
-            bound = max(1e-4, math.sqrt(2) * floor)
+            scale = exp.norm() + 1e-30
+            floor = max([((exp - e64).norm() / scale).item()] +
+                        [((u - exp).norm() / scale).item() for u in eu])
+            bound = max(1e-4, 2 * math.sqrt(2) * floor)
             dev = ((got - exp).norm() / scale).item()
-            dev64 = ((got - e64).norm() / s64).item()
-            ok = dev <= bound or dev64 <= max(1e-4, floor)
-            worst = max(worst, min(dev / bound, dev64 / max(1e-4, floor)))
-            assert ok, (f"{math_} {name}: {dev:.3g} from the fp32 oracle (bound {bound:.3g}), "
-                        f"{dev64:.3g} from float64 (reference fp32 x k: {floor:.3g})")
+            worst = max(worst, dev / bound)
+            assert dev <= bound, (f"{math_} {name}: {dev:.3g} from the fp32 oracle, bound {bound:.3g} "
+                                  f"(floor {floor:.3g})")
     assert math.isfinite(worst)
     print(f"cfg4 {math_} gradients: worst deviation {worst:.2f} of its bound")
