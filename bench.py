@@ -156,8 +156,8 @@ def _math():
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", choices=CONFIGS, default="cfg2",
                     help="BASELINE.json workload (cfg2 = the headline metric)")
     ap.add_argument("--batch", type=int, default=None, help="rays per rank per step")
