@@ -172,6 +172,9 @@ def _check_signature(part, group):
                        f"(keys / trailing shapes / dtypes): {sigs}")
 
 
+_CHECK_CALLS = {}   # sharded_map calls per process group (the signature check's schedule)
+
+
 def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None, check=True):
     """Row-sharded evaluation of ``fn`` over the ranks of ``group``: rank r
     applies ``fn`` to its contiguous slice of ``x`` (ceil(n / world) rows, the
@@ -182,9 +185,9 @@ def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None, check=True):
     rank's slice (e.g. a replay RNG holding the slice's random draws).
 
     Outputs that require grad stay differentiable: the gather's backward is a
-    reduce-scatter (``_GatherRows``).  ``check`` first compares the ranks' output
-    signatures (one 16-byte all-reduce of a digest) and raises on every rank if
-    they differ.
+    reduce-scatter (``_GatherRows``).  ``check`` compares the ranks' output
+    signatures (one 16-byte all-reduce of a digest) on the group's calls 1, 2,
+    4, 8, ... and raises on every rank if they differ.
 
     Used for config 5's light image (SURVEY 8e "phase 2"): the reference
     renders the full light image on every rank (train_efficient_sm.py:158-168);
@@ -201,7 +204,14 @@ def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None, check=True):
     else:       # an empty slice still takes part in every collective (same keys)
         part = fn(x[n - 1:n], **(rank_args(n - 1, n) if rank_args else {}))
     if check:
-        _check_signature(part, group)
+        # every rank makes the same sequence of sharded_map calls (the gathers
+        # below are collectives), so a per-group call count is the same on all
+        # of them: the signature is compared on calls 1, 2, 4, 8, ... -- a
+        # training loop pays one host sync per doubling, not one per step
+        key = id(group) if group is not None else None
+        c = _CHECK_CALLS[key] = _CHECK_CALLS.get(key, 0) + 1
+        if c & (c - 1) == 0:
+            _check_signature(part, group)
     out = {}
     for k in sorted(part):
         v = part[k]

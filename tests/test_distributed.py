@@ -278,6 +278,32 @@ def test_sharded_map_rejects_mismatched_outputs():
         assert status == "raised" and "different outputs" in msg, (rank, status, msg)
 
 
+def _check_schedule_worker(rank, world, port, q, calls):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nerf_pl_amd import distributed as D
+        checked = []
+        real = D._check_signature
+        D._check_signature = lambda part, group: (checked.append(len(checked)), real(part, group))
+        x = torch.arange(12, dtype=torch.float32).view(4, 3)
+        for _ in range(calls):
+            out = D.sharded_map(lambda xs: {"s": xs.sum(1)}, x)
+        q.put(_to_np(((rank, len(checked), out["s"]))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_map_checks_signatures_on_doubling_calls():
+    """the signature check's host sync runs on calls 1, 2, 4, 8 of a
+    group (the same calls on every rank), not on every training step"""
+    res = _run(2, _check_schedule_worker, 9)
+    for rank, n_checked, s in res:
+        assert n_checked == 4, (rank, n_checked)
+        torch.testing.assert_close(s, torch.arange(12, dtype=torch.float32).view(4, 3).sum(1))
+
+
 def _sampler_worker(rank, world, port, q, total, batch, steps):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
