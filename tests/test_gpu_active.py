@@ -60,11 +60,13 @@ def test_active_sample_list_empty_and_all_zero():
     assert _samples(torch.zeros(300, 4, device=DEV))[1] == 0
 
 
-def _mlp_grads(math, active, g_out_fn, monkeypatch, n=4096, spr=64, sigma_only=False, seed=5):
+def _mlp_grads(math, active, g_out_fn, monkeypatch, n=4096, spr=64, sigma_only=False, seed=5,
+               defer="none"):
     from nerf_pl_amd import NeRF, functions, ops
     from nerf_pl_amd.rays import blender_rays
     monkeypatch.setattr(ops, "MATH", math)
     monkeypatch.setattr(functions, "ACTIVE_SAMPLES", active)
+    monkeypatch.setattr(functions, "DEFER_SAVE", defer)
     m = NeRF()
     m.load_state_dict(O.make_params(seed, sigma_bias=0.3))
     m = m.to(DEV)
@@ -115,6 +117,29 @@ def test_active_backward_matches_every_sample(math, case, sigma_only, monkeypatc
     fn = _zeroed(case)
     a = _mlp_grads(math, True, fn, monkeypatch, sigma_only=sigma_only)
     b = _mlp_grads(math, False, fn, monkeypatch, sigma_only=sigma_only)
+    for k in b:
+        if b[k] is None:
+            assert a[k] is None, k
+            continue
+        if case == "none":
+            assert torch.count_nonzero(a[k]) == 0, k
+            continue
+        dev = ((a[k] - b[k]).norm() / (b[k].norm() + 1e-30)).item()
+        assert dev <= 2e-6, f"{math} {case} {k}: {dev:.3g}"
+
+
+@pytest.mark.parametrize("math", ["f16x3", "bf16x6", "fp32"])
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("sigma_only", [False, True])
+def test_deferred_backward_matches_every_sample(math, case, sigma_only, monkeypatch):
+    """the deferred save over every list shape, on a ragged
+    sample count (61 rays x 48 samples = 91.5 blocks of 32): the listed
+    re-run, data and weight gradients against the every-sample backward over a
+    forward-time save; an empty list (case "none") gives exact zeros"""
+    fn = _zeroed(case)
+    a = _mlp_grads(math, True, fn, monkeypatch, n=61 * 48, spr=48, sigma_only=sigma_only,
+                   defer="all")
+    b = _mlp_grads(math, False, fn, monkeypatch, n=61 * 48, spr=48, sigma_only=sigma_only)
     for k in b:
         if b[k] is None:
             assert a[k] is None, k
