@@ -61,9 +61,9 @@ def normed_depth(camera: torch.Tensor, pixels: torch.Tensor, depth: torch.Tensor
     """depth / (|camera @ pixel| + 1e-5) (:47-62, column 3); differentiable in
     ``depth`` (the light render's depths under --grad_on_light)."""
     dev = depth.device
-    pixels = ops._dev(pixels.to(dev, torch.float32), "pixels", 3)
+    pixels = ops._dev(ops.to_device_f32(pixels, dev), "pixels", 3)
     depth = ops._dev(depth.reshape(-1), "depth")
-    cam = ops._dev(camera.to(dev, torch.float32).reshape(9), "camera")
+    cam = ops._dev(ops.to_device_f32(camera, dev).reshape(9), "camera")
     if pixels.shape[0] != depth.shape[0]:
         raise ValueError(f"normed_depth: {pixels.shape[0]} pixels for {depth.shape[0]} depths")
     return _NormedDepth.apply(cam, pixels, depth)
@@ -128,9 +128,8 @@ def shadow_map(depth, pixels, eye, cams, light_eye, light_cam, normed_light_w, r
     dev = depth.device
     depth = ops._dev(depth.reshape(-1), "depth")
     n = depth.shape[0]
-    f32 = dict(device=dev, dtype=torch.float32)
-    pixels = ops._dev(pixels.to(**f32), "pixels", 3)
-    eye, cams = eye.to(**f32), cams.to(**f32)
+    pixels = ops._dev(ops.to_device_f32(pixels, dev), "pixels", 3)
+    eye, cams = ops.to_device_f32(eye, dev), ops.to_device_f32(cams, dev)
     per_ray = eye.dim() == 2 and eye.shape[0] == n and n > 1
     if per_ray:
         eye = eye.reshape(n, 3).contiguous()
@@ -143,8 +142,8 @@ def shadow_map(depth, pixels, eye, cams, light_eye, light_cam, normed_light_w, r
     if lw.shape[0] != w * h:
         raise ValueError(f"light depth map has {lw.shape[0]} entries, expected {w}x{h}")
     return _ShadowMap.apply(depth, pixels, eye, cams, per_ray,
-                            light_cam.to(**f32).reshape(9).contiguous(),
-                            light_eye.to(**f32).reshape(3).contiguous(), lw, (w, h),
+                            ops.to_device_f32(light_cam, dev).reshape(9).contiguous(),
+                            ops.to_device_f32(light_eye, dev).reshape(3).contiguous(), lw, (w, h),
                             _METHODS[mode], delta, epsilon, bool(sigmoid), out_eps)
 
 

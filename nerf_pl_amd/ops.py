@@ -69,6 +69,21 @@ def _dev(t: torch.Tensor, name: str, shape_last=None):
     return t
 
 
+def to_device_f32(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
+    """``t.to(dev, float32)`` without draining the stream: a host tensor (e.g.
+    the light camera the reference keeps on the CPU, train_efficient_sm.py)
+    is staged through pinned memory and copied asynchronously -- a pageable
+    ``.to(dev)`` returns only once the stream has run dry, which left the GPU
+    idle while the host queued the rest of the step.  The caching host
+    allocator keeps the pinned block alive until the copy has run."""
+    t = t.to(torch.float32)
+    if t.device == dev:
+        return t
+    if t.device.type == "cpu":
+        return t.contiguous().pin_memory().to(dev, non_blocking=True)
+    return t.to(dev)
+
+
 @functools.lru_cache(maxsize=None)
 def _maps(device_index: int):
     dev = torch.device("cuda", device_index)

@@ -137,10 +137,10 @@ def efficient_sm(cam_pixels, light_pixels, cam_results, light_results, ppc, ligh
     n = d_c.shape[0]
     eye, cams = _ppc_arrays(ppc, n)
     leye, lcam = _cam(light_ppc)
-    leye = leye.reshape(3).to(dev, torch.float32)
-    lcam = lcam.reshape(3, 3).to(dev, torch.float32)
-    cam_pixels = cam_pixels.to(dev, torch.float32)
-    light_pixels = light_pixels.to(dev, torch.float32).reshape(-1, 3)
+    leye = ops.to_device_f32(leye.reshape(3), dev)
+    lcam = ops.to_device_f32(lcam.reshape(3, 3), dev)
+    cam_pixels = ops.to_device_f32(cam_pixels, dev)
+    light_pixels = ops.to_device_f32(light_pixels, dev).reshape(-1, 3)
 
     light_c = normed_depth(lcam, light_pixels, light_results["depth_coarse"])
     sm_c = shadow_map(d_c, cam_pixels, eye, cams, leye, lcam, light_c, image_shape,
