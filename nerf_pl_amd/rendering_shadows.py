@@ -33,8 +33,9 @@ __all__ = ["render_rays", "render_rays_sharded", "efficient_sm"]
 
 
 def _disp(depth, opac):
-    # rendering_shadows.py:193
-    return 1. / torch.max(1e-10 * torch.ones_like(depth), depth / opac)
+    # rendering_shadows.py:193, 1 / max(1e-10 * ones, depth / opac): the same
+    # values (and NaN propagation) in three launches instead of five
+    return torch.reciprocal(torch.clamp_min(depth / opac, 1e-10))
 
 
 def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=0, noise_std=1,
