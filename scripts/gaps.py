@@ -9,9 +9,9 @@ import sys
 f = glob.glob(f"{sys.argv[1]}/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
-if len(ends) < 2:       # inference workloads: no optimizer; one window over the trace
-    ends = [0, len(rows) - 1]
-for a, b in zip(ends[-4:-1], ends[-3:]):
+if len(ends) < 2:       # inference workloads: no optimizer; a step starts at its ray generation
+    ends = [i - 1 for i, r in enumerate(rows) if "gen_rays_kernel" in r["Kernel_Name"] and i > 0]
+for a, b in list(zip(ends[:-1], ends[1:]))[-3:]:
     seg = rows[a + 1:b + 1]
     wall = (int(rows[b]["End_Timestamp"]) - int(rows[a]["End_Timestamp"])) / 1e6
     busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg) / 1e6
