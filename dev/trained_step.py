@@ -4,8 +4,9 @@ gradient; a NeRF that has learnt its scene leaves most samples in empty
 space or behind a surface, with an exactly zero gradient.  This times the
 cfg2-shaped step (4,096 rays, 64 + 128 samples, perturb 1, noise 1, MSE,
 Adam) on the PSNR scene's training views with weights trained by
-scripts/psnr_compare.py --save-weights, with and without the zero-gradient
-sample lists.
+scripts/psnr_compare.py --save-weights: the zero-gradient sample lists with
+the adaptive deferred save (NERF_PL_AMD_DEFER_SAVE=auto, the default), with a
+forward-time save (none), and the every-sample backward.
 
     python dev/trained_step.py <weights.safetensors> [--steps 20] [--out f.json]
 """
@@ -42,8 +43,10 @@ def main():
     sd = load_file(args.weights)
     emb = [Embedding(3, 10), Embedding(3, 4)]
     res = {"weights": os.path.basename(args.weights), "rays": 4096, "samples": [64, 128]}
-    for active in (True, False):
+    for mode in ("auto", "none", "every_sample"):
+        active = mode != "every_sample"
         functions.ACTIVE_SAMPLES = active
+        functions.DEFER_SAVE = mode if active else "none"
         models = []
         for tag in ("coarse", "fine"):
             m = NeRF()
@@ -78,8 +81,9 @@ def main():
             row["listed_fraction_fine"] = round(sum(fr[0::2]) / len(fr[0::2]), 4)
             row["listed_fraction_coarse"] = round(sum(fr[1::2]) / len(fr[1::2]), 4)
             functions.ACTIVE_LOG = None
-        res["active" if active else "every_sample"] = row
-        print(("active" if active else "every_sample"), json.dumps(row), flush=True)
+            row["deferred_last_step"] = [bool(m.__dict__.get("_nr_defer_last")) for m in models]
+        res[mode] = row
+        print(mode, json.dumps(row), flush=True)
     if args.out:
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)

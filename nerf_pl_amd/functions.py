@@ -49,12 +49,46 @@ ACTIVE_ARITHS = ("f16x3", "bf16x6", "fp32")
 # few samples runs without saving activations (the inference kernel), and the
 # backward re-evaluates the listed samples only, saving them by position
 # (nr_mlp_fwd_listed*) -- exact: the recomputed layers are the forward's layers
-# bit for bit.  "sigma" (default): the sigma-only graphs of the shadow path
-# (rendering_shadows.py:167), whose backward lists ~0.1% of a light image's
-# samples and ~20% of the camera rays'; "all": every training forward; "none"
-DEFER_SAVE = os.environ.get("NERF_PL_AMD_DEFER_SAVE", "sigma")
-if DEFER_SAVE not in ("sigma", "all", "none"):
-    raise ValueError(f"NERF_PL_AMD_DEFER_SAVE must be sigma, all or none, got {DEFER_SAVE!r}")
+# bit for bit, so every step's results are the same whichever way it goes.
+# "sigma": the sigma-only graphs of the shadow path (rendering_shadows.py:167),
+# whose backward lists ~0.1% of a light image's samples and ~20% of the camera
+# rays'; "all": every training forward; "none": none; "auto" (default): the
+# sigma-only graphs, and a full graph whenever its model's last backward listed
+# fewer than DEFER_AUTO of the samples (a trained NeRF leaves most samples in
+# empty space; at the bench's random init ~half are listed, where saving at
+# forward time is faster)
+DEFER_SAVE = os.environ.get("NERF_PL_AMD_DEFER_SAVE", "auto")
+if DEFER_SAVE not in ("sigma", "all", "none", "auto"):
+    raise ValueError(f"NERF_PL_AMD_DEFER_SAVE must be auto, sigma, all or none, got {DEFER_SAVE!r}")
+DEFER_AUTO = float(os.environ.get("NERF_PL_AMD_DEFER_AUTO", "0.3"))
+
+
+def _listed_fraction(model, sigma_only):
+    """the fraction of samples the model's last backward of this graph kind
+    listed, or None when not known yet.  The count is copied device -> pinned
+    host memory behind an event by that backward (_note_listed) and read only
+    once the event has completed: no synchronisation."""
+    st = model.__dict__.setdefault("_nr_listed", {})
+    e = st.get(sigma_only)
+    if e is None:
+        return None
+    frac, pending = e
+    if pending is not None and pending[1].query():
+        host, _, n = pending
+        frac = int(host[0]) / max(n, 1)
+        st[sigma_only] = (frac, None)
+    return frac
+
+
+def _note_listed(model, sigma_only, count_dev, n):
+    """queue the copy of a backward's sample-list length for _listed_fraction"""
+    host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+    host.copy_(count_dev, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    st = model.__dict__.setdefault("_nr_listed", {})
+    prev = st.get(sigma_only)
+    st[sigma_only] = (prev[0] if prev else None, (host, ev, n))
 # bench.py's kernel timer: a list every backward appends its (sample list
 # buffer, index of its length) to, so the rooflines count the samples worked on
 ACTIVE_LOG = None
@@ -82,8 +116,14 @@ class _FusedMLP(torch.autograd.Function):
         # xyz_encoding_final / dir / rgb work), in every arithmetic
         so_train = train and sigma_only and SIGMA_TRAIN_KERNELS and x is None
         kern_sigma_only = sigma_only and (not train or so_train)
-        defer = (train and x is None and ACTIVE_SAMPLES and ops.arith_of(packed_b) in ACTIVE_ARITHS
-                 and (DEFER_SAVE == "all" or (DEFER_SAVE == "sigma" and so_train)))
+        defer = False
+        if train and x is None and ACTIVE_SAMPLES and ops.arith_of(packed_b) in ACTIVE_ARITHS:
+            if DEFER_SAVE == "all" or (DEFER_SAVE in ("sigma", "auto") and so_train):
+                defer = True
+            elif DEFER_SAVE == "auto":
+                frac = _listed_fraction(model, sigma_only)
+                defer = frac is not None and frac < DEFER_AUTO
+        model.__dict__["_nr_defer_last"] = defer
         out, save = ops.mlp_forward(packed_f, rays=rays, z=z, samples_per_ray=spr, x=x,
                                     sigma_only=kern_sigma_only, save=train and not defer)
         if train:
@@ -94,6 +134,7 @@ class _FusedMLP(torch.autograd.Function):
                 ctx.save_for_backward(out, save, packed_f, packed_b)
             ctx.defer = defer
             ctx.sigma_only = sigma_only
+            ctx.model = model if DEFER_SAVE == "auto" else None
             ctx.so_kernels = so_train
         if sigma_only and train and out.shape[1] == 4:
             out = out[:, 3:4].contiguous()
@@ -124,6 +165,8 @@ class _FusedMLP(torch.autograd.Function):
             active = (sl.data_ptr(), sl.data_ptr() + 4 * n)
             if ACTIVE_LOG is not None:
                 ACTIVE_LOG.append((sl, n))
+            if ctx.model is not None:
+                _note_listed(ctx.model, ctx.sigma_only, sl[n:n + 1], n)
             sfx += "_active"
         call(ops.entry("nr_mlp_bwd" + sfx, packed_b), packed_b.data_ptr(), ops.head_ptr(packed_f),
              out.data_ptr(), g_out.data_ptr(), save.data_ptr(), n, grad_ws.data_ptr(), *active, st)
@@ -158,6 +201,8 @@ class _FusedMLP(torch.autograd.Function):
         lst = (sl.data_ptr(), sl.data_ptr() + 4 * n)
         if ACTIVE_LOG is not None:
             ACTIVE_LOG.append((sl, n))
+        if ctx.model is not None:
+            _note_listed(ctx.model, ctx.sigma_only, sl[n:n + 1], n)
         so = ctx.so_kernels
         save = torch.empty(ops.save_floats(n), device=dev)
         call(ops.entry("nr_mlp_fwd_listed", packed_f), packed_f.data_ptr(), rays.data_ptr(),

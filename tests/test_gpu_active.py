@@ -151,6 +151,48 @@ def test_deferred_backward_matches_every_sample(math, case, sigma_only, monkeypa
         assert dev <= 2e-6, f"{math} {case} {k}: {dev:.3g}"
 
 
+@pytest.mark.parametrize("math", ["f16x3", "bf16x6", "fp32"])
+def test_auto_defer_follows_the_listed_fraction(math, monkeypatch):
+    """NERF_PL_AMD_DEFER_SAVE=auto (the default): a model's full-graph forward
+    defers its save once the model's last backward listed fewer than
+    DEFER_AUTO of the samples, and goes back to the forward-time save when a
+    backward lists many; every step's gradients equal the forward-time save's
+    bit for bit"""
+    from nerf_pl_amd import NeRF, functions, ops
+    from nerf_pl_amd.rays import blender_rays
+    monkeypatch.setattr(ops, "MATH", math)
+    monkeypatch.setattr(functions, "ACTIVE_SAMPLES", True)
+    spr, nr = 64, 48
+    rays = blender_rays(32, 1, near=2.0, far=6.0)[:nr].contiguous().to(DEV)
+    g = torch.Generator().manual_seed(3)
+    z = (2.0 + 4.0 * torch.rand(nr, spr, generator=g)).sort(1).values.to(DEV)
+    models = {}
+    for k in ("auto", "none"):
+        m = NeRF()
+        m.load_state_dict(O.make_params(8, sigma_bias=0.3))
+        models[k] = m.to(DEV)
+
+    def step(kind, case, seed):
+        monkeypatch.setattr(functions, "DEFER_SAVE", kind)
+        m = models[kind]
+        for p in m.parameters():
+            p.grad = None
+        out = functions.mlp_apply(m, rays=rays, z=z, spr=spr)
+        out.backward(_zeroed(case)(out.shape, torch.Generator().manual_seed(seed)).to(DEV))
+        torch.cuda.synchronize()
+        return [p.grad.detach().clone() for p in m.parameters()], m.__dict__["_nr_defer_last"]
+
+    seen = []
+    for i, case in enumerate(("one", "one", "dense", "dense", "scattered")):
+        ga, deferred = step("auto", case, 40 + i)
+        gb, _ = step("none", case, 40 + i)
+        seen.append(deferred)
+        for a, b in zip(ga, gb):
+            assert torch.equal(a, b), (math, i, case)
+    # no statistics yet; 1 of 3072 listed; still following step 1; all listed; ~half
+    assert seen == [False, True, True, False, False], seen
+
+
 @pytest.mark.parametrize("math", ["f16x3", "fp32"])
 def test_deferred_save_full_graph(math, monkeypatch):
     """NERF_PL_AMD_DEFER_SAVE=all on the full graph (render_rays' training
