@@ -865,7 +865,9 @@ def main():
     # size (coarse / fine pass), over the timed steps
     from nerf_pl_amd import functions as _functions
     backward_blocks = dict(skip_zero_gradient_samples=bool(_functions.ACTIVE_SAMPLES
-                                                           and math_main in _functions.ACTIVE_ARITHS))
+                                                           and math_main in _functions.ACTIVE_ARITHS),
+                           deferred_save=_functions.DEFER_SAVE,
+                           deferred_save_threshold=_functions.DEFER_AUTO)
     for k in ("mlp_bwd_dgrad", "mlp_bwd_dgrad_sigma"):
         evs = timer.events.get(k, [])
         if evs and any(ev[3] is not None for ev in evs):
