@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--modes", default="auto,none,every_sample",
+                    help="DEFER_SAVE settings to time (auto, all, none, sigma) and/or every_sample")
     args = ap.parse_args()
     import psnr_compare as pc
     from safetensors.torch import load_file
@@ -43,7 +45,7 @@ def main():
     sd = load_file(args.weights)
     emb = [Embedding(3, 10), Embedding(3, 4)]
     res = {"weights": os.path.basename(args.weights), "rays": 4096, "samples": [64, 128]}
-    for mode in ("auto", "none", "every_sample"):
+    for mode in args.modes.split(","):
         active = mode != "every_sample"
         functions.ACTIVE_SAMPLES = active
         functions.DEFER_SAVE = mode if active else "none"

@@ -9,6 +9,7 @@ per ``NeRF`` parameter (views into one flat buffer, named_parameters order).
 """
 from __future__ import annotations
 
+import collections
 import functools
 import os
 
@@ -64,20 +65,21 @@ DEFER_AUTO = float(os.environ.get("NERF_PL_AMD_DEFER_AUTO", "0.3"))
 
 
 def _listed_fraction(model, sigma_only):
-    """the fraction of samples the model's last backward of this graph kind
-    listed, or None when not known yet.  The count is copied device -> pinned
-    host memory behind an event by that backward (_note_listed) and read only
-    once the event has completed: no synchronisation."""
+    """the fraction of samples the model's latest completed backward of this
+    graph kind listed, or None when none has completed yet.  Each backward
+    queues a device -> pinned host copy of its list length behind an event
+    (_note_listed); this reads the copies whose events have completed, oldest
+    first (one stream: they complete in order) -- no synchronisation, and a
+    host running several steps ahead of the GPU still sees the newest finished
+    count."""
     st = model.__dict__.setdefault("_nr_listed", {})
     e = st.get(sigma_only)
     if e is None:
         return None
-    frac, pending = e
-    if pending is not None and pending[1].query():
-        host, _, n = pending
-        frac = int(host[0]) / max(n, 1)
-        st[sigma_only] = (frac, None)
-    return frac
+    while e[1] and e[1][0][1].query():
+        host, _, n = e[1].popleft()
+        e[0] = int(host[0]) / max(n, 1)
+    return e[0]
 
 
 def _note_listed(model, sigma_only, count_dev, n):
@@ -86,9 +88,13 @@ def _note_listed(model, sigma_only, count_dev, n):
     host.copy_(count_dev, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
-    st = model.__dict__.setdefault("_nr_listed", {})
-    prev = st.get(sigma_only)
-    st[sigma_only] = (prev[0] if prev else None, (host, ev, n))
+    e = model.__dict__.setdefault("_nr_listed", {}).setdefault(
+        sigma_only, [None, collections.deque()])
+    e[1].append((host, ev, n))
+    if len(e[1]) > 16:       # a host far ahead: the oldest copies are not needed
+        e[1].popleft()
+
+
 # bench.py's kernel timer: a list every backward appends its (sample list
 # buffer, index of its length) to, so the rooflines count the samples worked on
 ACTIVE_LOG = None
