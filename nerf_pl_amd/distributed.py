@@ -158,8 +158,11 @@ def _check_signature(part, group):
     # 63-bit digest of the signature) instead of pickling every rank's
     # signature through all_gather_object; that runs only to report a mismatch
     h = int.from_bytes(hashlib.blake2b(repr(sig).encode(), digest_size=8).digest(), "little") >> 1
-    dev = next((v.device for v in part.values() if v is not None), torch.device("cpu"))
-    if dist.get_backend(group) == "gloo":
+    # the device follows the backend, not the outputs (a part whose
+    # values are all None must still reduce on the device NCCL needs)
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
         dev = torch.device("cpu")
     t = torch.tensor([h, -h], dtype=torch.int64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
@@ -170,9 +173,6 @@ def _check_signature(part, group):
     dist.all_gather_object(sigs, sig, group=group)
     raise RuntimeError("sharded_map: ranks produced different outputs "
                        f"(keys / trailing shapes / dtypes): {sigs}")
-
-
-_CHECK_CALLS = {}   # sharded_map calls per process group (the signature check's schedule)
 
 
 def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None, check=True):
@@ -186,8 +186,11 @@ def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None, check=True):
 
     Outputs that require grad stay differentiable: the gather's backward is a
     reduce-scatter (``_GatherRows``).  ``check`` compares the ranks' output
-    signatures (one 16-byte all-reduce of a digest) on the group's calls 1, 2,
-    4, 8, ... and raises on every rank if they differ.
+    signatures (one 16-byte all-reduce of a digest) on every call, before any
+    output is gathered, and raises on every rank if they differ: the key set
+    can change from step to step (train_efficient_sm.py:153-154 draws
+    Light_N_importance per step), so a check on some calls only would let a
+    divergent step pair different tensors in the gathers or hang.
 
     Used for config 5's light image (SURVEY 8e "phase 2"): the reference
     renders the full light image on every rank (train_efficient_sm.py:158-168);
@@ -204,14 +207,9 @@ def sharded_map(fn, x: torch.Tensor, group=None, rank_args=None, check=True):
     else:       # an empty slice still takes part in every collective (same keys)
         part = fn(x[n - 1:n], **(rank_args(n - 1, n) if rank_args else {}))
     if check:
-        # every rank makes the same sequence of sharded_map calls (the gathers
-        # below are collectives), so a per-group call count is the same on all
-        # of them: the signature is compared on calls 1, 2, 4, 8, ... -- a
-        # training loop pays one host sync per doubling, not one per step
-        key = id(group) if group is not None else None
-        c = _CHECK_CALLS[key] = _CHECK_CALLS.get(key, 0) + 1
-        if c & (c - 1) == 0:
-            _check_signature(part, group)
+        # one 16-byte all-reduce and a host read of it per call: measured
+        # against the light render it guards, a few tens of microseconds
+        _check_signature(part, group)
     out = {}
     for k in sorted(part):
         v = part[k]

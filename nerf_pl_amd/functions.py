@@ -12,6 +12,8 @@ from __future__ import annotations
 import collections
 import functools
 import os
+import threading
+import weakref
 
 import torch
 
@@ -64,6 +66,23 @@ if DEFER_SAVE not in ("sigma", "all", "none", "auto"):
 DEFER_AUTO = float(os.environ.get("NERF_PL_AMD_DEFER_AUTO", "0.3"))
 
 
+# Per-model statistics of the deferred-save policy: model -> {sigma_only:
+# _ListedStats}.  Kept outside the module (a WeakKeyDictionary: an entry dies
+# with its model) so a NeRF stays deep-copyable and picklable after training
+# steps -- the entries hold CUDA events, which cannot be pickled.
+_LISTED = weakref.WeakKeyDictionary()
+_LISTED_LOCK = threading.Lock()
+
+
+class _ListedStats:
+    """the latest completed list fraction and the copies still in flight"""
+    __slots__ = ("frac", "pending")
+
+    def __init__(self):
+        self.frac = None
+        self.pending = collections.deque()     # (pinned host count, event, n), oldest first
+
+
 def _listed_fraction(model, sigma_only):
     """the fraction of samples the model's latest completed backward of this
     graph kind listed, or None when none has completed yet.  Each backward
@@ -71,15 +90,20 @@ def _listed_fraction(model, sigma_only):
     (_note_listed); this reads the copies whose events have completed, oldest
     first (one stream: they complete in order) -- no synchronisation, and a
     host running several steps ahead of the GPU still sees the newest finished
-    count."""
-    st = model.__dict__.setdefault("_nr_listed", {})
-    e = st.get(sigma_only)
-    if e is None:
-        return None
-    while e[1] and e[1][0][1].query():
-        host, _, n = e[1].popleft()
-        e[0] = int(host[0]) / max(n, 1)
-    return e[0]
+    count.  All trimming happens here, under the lock, and an entry is popped
+    only after its own event was seen complete (a backward on
+    another thread can append concurrently)."""
+    with _LISTED_LOCK:
+        e = _LISTED.get(model, {}).get(sigma_only)
+        if e is None:
+            return None
+        while e.pending and e.pending[0][1].query():
+            host, _, n = e.pending.popleft()
+            e.frac = int(host[0]) / max(n, 1)
+        # a host far ahead of the GPU: keep the newest 16 copies in flight
+        while len(e.pending) > 16:
+            e.pending.popleft()
+        return e.frac
 
 
 def _note_listed(model, sigma_only, count_dev, n):
@@ -88,11 +112,11 @@ def _note_listed(model, sigma_only, count_dev, n):
     host.copy_(count_dev, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record()
-    e = model.__dict__.setdefault("_nr_listed", {}).setdefault(
-        sigma_only, [None, collections.deque()])
-    e[1].append((host, ev, n))
-    if len(e[1]) > 16:       # a host far ahead: the oldest copies are not needed
-        e[1].popleft()
+    with _LISTED_LOCK:
+        per_model = _LISTED.get(model)
+        if per_model is None:
+            per_model = _LISTED[model] = {}
+        per_model.setdefault(sigma_only, _ListedStats()).pending.append((host, ev, n))
 
 
 # bench.py's kernel timer: a list every backward appends its (sample list
@@ -130,6 +154,11 @@ class _FusedMLP(torch.autograd.Function):
                 frac = _listed_fraction(model, sigma_only)
                 defer = frac is not None and frac < DEFER_AUTO
         model.__dict__["_nr_defer_last"] = defer
+        if x is None:
+            # the tensors the kernels read (contiguous copies of strided views):
+            # the deferred backward re-reads exactly these
+            rays = ops._dev(rays, "rays", 8)
+            z = ops._dev(z, "z")
         out, save = ops.mlp_forward(packed_f, rays=rays, z=z, samples_per_ray=spr, x=x,
                                     sigma_only=kern_sigma_only, save=train and not defer)
         if train:

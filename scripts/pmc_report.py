@@ -1,4 +1,4 @@
-"""Summarise scripts/pmc.sh output per kernel (dev tool): pmc_report.py <dir>"""
+"""Summarise rocprofv3 --pmc pass directories per kernel (dev tool): pmc_report.py <dir>"""
 import collections
 import csv
 import glob

@@ -1,4 +1,4 @@
-"""Per-kernel limiter report from scripts/prof_r04.sh's counter passes over
+"""Per-kernel limiter report from scripts/gpu.sh sq (round 4: prof_r04.sh) counter passes over
 bench.py's own training step (dev tool).
 
     python scripts/sq_report.py gpurun_out/r04/<tag> [out.json]

@@ -1,4 +1,4 @@
-"""Per-launch HBM traffic of the fused kernels from scripts/pmc.sh output
+"""Per-launch HBM traffic of the fused kernels from rocprofv3 --pmc pass directories (scripts/gpu.sh traffic)
 (dev tool): traffic.py <pmc dir> <out json> [--x3 | --arith f16x3 [--fwd-save-only]].
 
 --arith NAME keeps the split-operand kernels only, stores the entries under

@@ -278,29 +278,41 @@ def test_sharded_map_rejects_mismatched_outputs():
         assert status == "raised" and "different outputs" in msg, (rank, status, msg)
 
 
-def _check_schedule_worker(rank, world, port, q, calls):
+def _check_schedule_worker(rank, world, port, q, calls, diverge_at):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from nerf_pl_amd import distributed as D
-        checked = []
-        real = D._check_signature
-        D._check_signature = lambda part, group: (checked.append(len(checked)), real(part, group))
         x = torch.arange(12, dtype=torch.float32).view(4, 3)
-        for _ in range(calls):
-            out = D.sharded_map(lambda xs: {"s": xs.sum(1)}, x)
-        q.put(_to_np(((rank, len(checked), out["s"]))))
+        out = None
+        for c in range(1, calls + 1):
+            def fn(xs, c=c):
+                r = {"s": xs.sum(1)}
+                if c == diverge_at and rank == 1:     # this rank drew a different N_importance
+                    r["extra"] = xs
+                return r
+            try:
+                out = D.sharded_map(fn, x)
+            except RuntimeError as e:
+                q.put(_to_np((rank, "raised", c, str(e))))
+                return
+        q.put(_to_np((rank, "ok", calls, out["s"])))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_map_checks_signatures_on_doubling_calls():
-    """the signature check's host sync runs on calls 1, 2, 4, 8 of a
-    group (the same calls on every rank), not on every training step"""
-    res = _run(2, _check_schedule_worker, 9)
-    for rank, n_checked, s in res:
-        assert n_checked == 4, (rank, n_checked)
+def test_sharded_map_checks_signatures_on_every_call():
+    """the key set may change between steps (a per-step
+    Light_N_importance draw), so the signature is compared on every call:
+    ranks that diverge at call 3 -- not a power of two -- raise there, on
+    every rank, before any gather pairs different tensors"""
+    res = _run(2, _check_schedule_worker, 6, 3)
+    for rank, status, c, msg in res:
+        assert status == "raised" and c == 3 and "different outputs" in msg, (rank, status, c)
+    res = _run(2, _check_schedule_worker, 5, -1)
+    for rank, status, c, s in res:
+        assert status == "ok" and c == 5
         torch.testing.assert_close(s, torch.arange(12, dtype=torch.float32).view(4, 3).sum(1))
 
 

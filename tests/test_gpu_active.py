@@ -264,3 +264,68 @@ def test_active_backward_in_render_rays(monkeypatch):
         for a, b in zip(ga, gb):
             dev = ((a - b).norm() / (b.norm() + 1e-30)).item()
             assert dev <= 1e-6, dev
+
+
+def test_nerf_copies_after_auto_defer_backward(monkeypatch):
+    """the auto deferral's per-model statistics (CUDA events) live
+    outside the module, so after training steps a NeRF still deep-copies,
+    pickles (torch.save) and wraps in AveragedModel, and the copy keeps no
+    statistics of its own"""
+    import copy
+    import io
+    from nerf_pl_amd import NeRF, functions, ops
+    from nerf_pl_amd.rays import blender_rays
+    monkeypatch.setattr(ops, "MATH", "f16x3")
+    monkeypatch.setattr(functions, "ACTIVE_SAMPLES", True)
+    monkeypatch.setattr(functions, "DEFER_SAVE", "auto")
+    spr, nr = 64, 16
+    rays = blender_rays(32, 1, near=2.0, far=6.0)[:nr].contiguous().to(DEV)
+    z = (2.0 + 4.0 * torch.rand(nr, spr, generator=torch.Generator().manual_seed(1))).sort(1).values.to(DEV)
+    m = NeRF()
+    m.load_state_dict(O.make_params(3, sigma_bias=0.3))
+    m = m.to(DEV)
+    for i in range(3):
+        out = functions.mlp_apply(m, rays=rays, z=z, spr=spr)
+        out.backward(_zeroed("one")(out.shape, torch.Generator().manual_seed(i)).to(DEV))
+    torch.cuda.synchronize()
+    assert functions._listed_fraction(m, False) is not None
+    c = copy.deepcopy(m)
+    buf = io.BytesIO()
+    torch.save(m, buf)
+    torch.optim.swa_utils.AveragedModel(m)
+    assert functions._listed_fraction(c, False) is None
+    for a, b in zip(m.parameters(), c.parameters()):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("math", ["f16x3", "fp32"])
+def test_deferred_save_strided_inputs(math, monkeypatch):
+    """ADVICE r4: a direct mlp_apply caller passing strided rays / depth views;
+    the deferred backward re-runs the forward on the very (contiguous) tensors
+    the forward read, so its gradients equal the forward-time save's bit for bit"""
+    from nerf_pl_amd import NeRF, functions, ops
+    from nerf_pl_amd.rays import blender_rays
+    monkeypatch.setattr(ops, "MATH", math)
+    monkeypatch.setattr(functions, "ACTIVE_SAMPLES", True)
+    spr, nr = 64, 48
+    rays = blender_rays(32, 1, near=2.0, far=6.0)[:nr].contiguous()
+    z = (2.0 + 4.0 * torch.rand(nr, spr, generator=torch.Generator().manual_seed(2))).sort(1).values
+    rbig = torch.full((nr, 16), float("nan"))
+    rbig[:, ::2] = rays
+    zbig = torch.full((nr, 2 * spr), float("nan"))
+    zbig[:, 1::2] = z
+    rv, zv = rbig.to(DEV)[:, ::2], zbig.to(DEV)[:, 1::2]
+    assert not rv.is_contiguous() and not zv.is_contiguous()
+    go = _zeroed("scattered")((nr * spr, 4), torch.Generator().manual_seed(4)).to(DEV)
+    grads = []
+    for defer, (r, zz) in (("all", (rv, zv)), ("none", (rays.to(DEV), z.to(DEV)))):
+        monkeypatch.setattr(functions, "DEFER_SAVE", defer)
+        m = NeRF()
+        m.load_state_dict(O.make_params(6, sigma_bias=0.3))
+        m = m.to(DEV)
+        out = functions.mlp_apply(m, rays=r, z=zz, spr=spr)
+        out.backward(go)
+        torch.cuda.synchronize()
+        grads.append([p.grad.detach().clone() for p in m.parameters()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)

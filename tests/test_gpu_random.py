@@ -9,22 +9,24 @@ cases (tests/test_gpu_render.py).  The reference's five draws are replayed in
 its order.  ``sample_pdf`` bin flips (u within ~1e-6 of a CDF knot,
 tests/test_gpu_render.py) are screened per ray and must stay rare.
 
-Gradient cases: the parameter gradient of a random linear functional of every
-output against oracle autograd.  This gradient is ill-conditioned in fp32 by
-construction -- xyz = o + d*z carries an fp32 rounding that the 2^9
-positional-encoding frequency turns into ~1e-3 rad of phase at |xyz| ~ 30,
-and ReLU kinks within an ulp of zero pick branches by summation order -- so
-the same oracle evaluated in float64 differs from its own fp32 result by up to
-5e-3 of a tensor's norm (median ~7e-4).  The bound: every gradient tensor is
-as close to the fp32 oracle as max(1e-4, that tensor's fp32-vs-float64
-distance of the oracle), normwise, with the rays whose importance samples
-differ (bin flips, here or in float64) out of the functional.
+Gradient cases (f16x3 and exact fp32): the parameter gradient of a random
+linear functional of every output against the float64 oracle.  This gradient
+is ill-conditioned in fp32 by construction -- xyz = o + d*z carries an fp32
+rounding that the 2^9 positional-encoding frequency turns into ~1e-3 rad of
+phase at |xyz| ~ 30, and ReLU kinks within an ulp of zero pick branches by
+summation order -- so the oracle's own fp32 result sits up to 5e-3 of a
+tensor's norm from float64 (median ~7e-4).  The bound (tests/grad64.py):
+every tensor within max(1e-4, 2 x that fp32 distance) of float64, normwise,
+the fp32 distance the largest at the weights and at two points one fp32 ulp
+away, with the rays whose importance samples differ (bin flips, here or in
+float64) out of the functional.
 """
 import numpy as np
 import pytest
 import torch
 
 from oracle import nerf_oracle as O
+import grad64
 from screening import pdf_flips
 
 pytestmark = pytest.mark.gpu
@@ -125,10 +127,14 @@ def test_random_config_matches_oracle(seed, math, monkeypatch):
         assert ok.all(), f"{k}: max err {err[~bad].max():.3g} on {int((~ok).sum())} rays, {c}"
 
 
-def _oracle_grads(c, rays, draws, dt):
-    params = [{k: v.to(dt).requires_grad_(True) for k, v in p.items()}
-              for p in (O.make_params(21 + c["seed"] % 5, sigma_bias=0.5),
-                        O.make_params(22 + c["seed"] % 5, sigma_bias=0.5))]
+def _oracle_grads(c, rays, draws, dt, ulp=None):
+    """the case's NeRF pair (optionally one fp32 ulp away, tests/grad64.py)
+    through the oracle in dtype dt"""
+    params = []
+    for s in (21 + c["seed"] % 5, 22 + c["seed"] % 5):
+        p = O.make_params(s, sigma_bias=0.5)
+        p = {k: v.to(dt) for k, v in p.items()} if ulp is None else grad64.ulp_perturbed(p, ulp + s, dt)
+        params.append({k: v.requires_grad_(True) for k, v in p.items()})
     cap = {}
     args = (c["S"], c["use_disp"], c["perturb"], c["noise"], c["I"], 32768, c["white_back"], False)
     ref = O.render_rays(params, rays.to(dt), *args, rng=O.ReplayRNG([d.to(dt) for d in draws]),
@@ -145,31 +151,51 @@ def _functional(out, keep, seed):
     return tot
 
 
-@pytest.mark.parametrize("seed", [101, 102, 103, 104, 105])
-def test_random_config_gradients_match_oracle(seed):
+def _zflips(c, cap32, cap64):
+    if c["I"] == 0:
+        return np.zeros(c["n"], bool)
+    z32, z64 = cap32["z_fine"].detach().double(), cap64["z_fine"].detach()
+    return ((z32 - z64).abs().max(1).values > 1e-4 * z64.abs().max(1).values.clamp(min=1)).numpy()
+
+
+def _named(models_or_params, zeros_like=None):
+    out = {}
+    for i, m in enumerate(models_or_params):
+        items = m.named_parameters() if hasattr(m, "named_parameters") else m.items()
+        for k, v in items:
+            g = v.grad
+            out[f"m{i}.{k}"] = (torch.zeros(v.shape, dtype=torch.float64) if g is None
+                                else g.detach().cpu().double())
+    return out
+
+
+@pytest.mark.parametrize("seed,math", [(s, m) for m in ("f16x3", "fp32")
+                                       for s in (101, 102, 103, 104, 105)])
+def test_random_config_gradients_match_oracle(seed, math, monkeypatch):
+    """every parameter gradient within max(1e-4, 2 x the fp32 oracle's own
+    distance from float64) of the float64 oracle (tests/grad64.py)"""
+    from nerf_pl_amd import ops
+    monkeypatch.setattr(ops, "MATH", math)
     c = _config(seed)
     c["test_time"] = False
     c["n"] = max(c["n"], 64)
-    models, params, res, ref, bad = _run(c, grad=True)
+    models, _, res, _, bad = _run(c, grad=True)
     rays, draws = _rays(c), _draws(c)
-    p64, ref64, cap64 = _oracle_grads(c, rays, draws, torch.float64)
-    if c["I"] > 0:        # importance samples that differ in float64 (bin flips) are screened too
-        _, _, cap32 = _oracle_grads(c, rays, draws, torch.float32)
-        z32, z64 = cap32["z_fine"].detach().double(), cap64["z_fine"].detach()
-        bad = bad | ((z32 - z64).abs().max(1).values > 1e-4 * z64.abs().max(1).values.clamp(min=1)).numpy()
+    pts = {u: (_oracle_grads(c, rays, draws, torch.float32, u), _oracle_grads(c, rays, draws, torch.float64, u))
+           for u in (None, 1, 2)}
+    (_, _, cap32), (_, _, cap64) = pts[None]
+    bad = bad | _zflips(c, cap32, cap64)   # importance samples that differ in float64 are screened too
     keep = torch.from_numpy(~bad)
     assert bad.sum() <= max(1, 0.05 * c["n"]), f"{bad.sum()} rays screened, {c}"
     _functional(res, keep, seed).backward()
-    _functional(ref, keep, seed).backward()
-    _functional(ref64, keep, seed).backward()
-    for m, p, q in zip(models, params, p64):
-        for name, w in m.named_parameters():
-            z = torch.zeros(w.shape, dtype=torch.float64)
-            exp = p[name].grad.double() if p[name].grad is not None else z
-            e64 = q[name].grad if q[name].grad is not None else z
-            got = w.grad.detach().cpu().double() if w.grad is not None else z
-            scale = exp.norm() + 1e-30
-            bound = max(1e-4, ((exp - e64).norm() / scale).item())
-            dev = ((got - exp).norm() / scale).item()
-            print(f"{seed} {name}: {dev:.3g} (bound {bound:.3g})")
-            assert dev <= bound, f"{name}: normwise deviation {dev:.3g} > {bound:.3g}, {c}"
+    g32s, g64s = [], []
+    for u, ((p32, r32, k32), (p64, r64, k64)) in pts.items():
+        if (_zflips(c, k32, k64) & ~bad).any():
+            continue            # a bin flip only at this ulp point: not a floor sample
+        _functional(r32, keep, seed).backward()
+        _functional(r64, keep, seed).backward()
+        g32s.append(_named(p32))
+        g64s.append(_named(p64))
+    floor = grad64.fp32_floor(g32s, g64s)
+    worst, where = grad64.check(_named(models), _named(pts[None][1][0]), floor, label=f"{seed} {math} {c}")
+    print(f"{seed} {math}: worst {worst:.2f} of its bound ({where}, fp32 floor {floor[where]:.3g})")
