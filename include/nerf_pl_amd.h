@@ -288,10 +288,17 @@ int nr_mlp_bwd(const float* packed_bwd, const float* head, const float* out,
 
 /* MLP backward, weight gradients: sum over all n samples of dz^T x for every
  * layer (split over workgroups, reduced in a fixed order), written as
- * d(loss)/d(params) into grad_flat (595,844 floats, named_parameters order). */
+ * d(loss)/d(params) into grad_flat (595,844 floats, named_parameters order).
+ * The forward does not save xyz_encoding_final's output (feat): every
+ * nr_wgrad* entry point of the full graph leaves G = sum dz_dir h8^T in
+ * dir_encoding.0.weight's first 256 columns, and nr_wgrad_dir_feat, given the
+ * flat fp32 parameters the forward ran with, turns them into the gradient
+ * G W_final^T + d(bias_dir) b_final^T (feat = W_final h8 + b_final,
+ * nerf.py:116-118; replaces autograd's sum dz_dir feat^T). */
 int64_t nr_wgrad_workspace_bytes(int64_t n);
 int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
              float* grad_flat, void* stream);
+int nr_wgrad_dir_feat(const float* params, float* grad_flat, void* stream);
 /* The same weight gradients on bf16x6 split-operand MFMA (fp32-level accuracy). */
 int nr_wgrad_x3(const float* save, const float* grad_ws, int64_t n, float* workspace,
                 float* grad_flat, void* stream);

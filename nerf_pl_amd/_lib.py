@@ -84,6 +84,7 @@ SIGNATURES = {
     "nr_wgrad_listed_h3": [_p, _p, _i64, _p, _p, _p, _p, _p],
     "nr_wgrad_sigma_listed_h3": [_p, _p, _i64, _p, _p, _p, _p, _p],
     "nr_wgrad_workspace_bytes": [_i64],
+    "nr_wgrad_dir_feat": [_p, _p, _p],
     "nr_sm_workspace_bytes": [_i64, _i64],
     "nr_wgrad": [_p, _p, _i64, _p, _p, _p],
     "nr_coarse_z": [_p, _p, _i64, _i, _i, _f, _p, _u64, _p, _p],

@@ -198,6 +198,27 @@ __device__ __forceinline__ void store_native_piece(const f32x16 (&acc)[NT], int 
     f32x4 v = {acc[t][4 * q + 0], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
     *reinterpret_cast<f32x4*>(blk + (p * 64 + lane) * 4) = v;
 }
+// NR_F32_ROWS (A/B knob): the exact-fp32 full-graph forward saves rows
+#ifndef NR_F32_ROWS
+#define NR_F32_ROWS 1
+#endif
+// piece p (= 4t + q) of a width-W activation as sample-major rows (the fp32
+// full-graph training save, like x3.h store_row): lane (h, j) holds features
+// 32t + 8q + 4h .. +3 of sample j (nr_acc_row), stored at row j of the block's
+// 32 rows of W floats, so the weight gradient can gather a sample's row whole
+template <int NT>
+__device__ __forceinline__ void store_row_piece(const f32x16 (&acc)[NT], int p, int W,
+                                                float* __restrict__ rows, int lane) {
+    const int t = p >> 2, q = p & 3;
+    f32x4 v = {acc[t][4 * q + 0], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+    *reinterpret_cast<f32x4*>(rows + (lane & 31) * W + 32 * t + 8 * q + 4 * (lane >> 5)) = v;
+}
+template <int NT>
+__device__ __forceinline__ void store_rows(const f32x16 (&acc)[NT], float* __restrict__ rows, int lane) {
+#pragma unroll
+    for (int p = 0; p < 4 * NT; ++p) store_row_piece<NT>(acc, p, 32 * NT, rows, lane);
+}
+
 template <int NT>
 __device__ __forceinline__ void store_native(const f32x16 (&acc)[NT], float* __restrict__ blk,
                                              int lane) {

@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
     __builtin_amdgcn_s_barrier();                       // head visible to every wave
     const uint4* mask = smask + lane;                   // [layer * 64]
     const float* H = Hs;
-    Frag f0;                                            // tile-0 fragments of the next k-group
+    Ahead f0;                                           // the first tiles' fragments of the next k-group
     enter<BwdTab, 0, QE>(smem, lane, f0);
 
     float dzr[2][3], dsig[2];

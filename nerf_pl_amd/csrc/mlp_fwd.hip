@@ -111,10 +111,16 @@ struct FwdArgs {
 };
 
 // LIST: the deferred save of a training forward (mlp_fwd3.hip);
-// blk is then a block of positions
+// blk is then a block of positions.  The full graph saves its activations as
+// sample-major rows (layout.h store_row_piece; PE and dir PE rows hold the
+// packed k order, column 32h + g / 16h + g), so the weight gradient of a
+// sample list gathers whole 128-B lines (the block-native
+// layout made it fetch 1.69x the listed samples' bytes); the sigma-only
+// training forward keeps the block-native layout
 template <int MODE, bool SIGMA_ONLY, bool LIST = false>
 __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     constexpr bool EMB = MODE == FWD_EMB;
+    constexpr bool ROWS = NR_F32_ROWS && !SIGMA_ONLY;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int h = lane >> 5;
@@ -172,7 +178,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
     auto side_acc8 = [&](const f32x16 (&X)[8], float* dst, uint32_t* msk) {
         return [&X, dst, msk, save, lane](int grp) {
             if (!save) return;
-            if (grp < 32) store_native_piece<8>(X, grp, dst, lane);
+            if (grp < 32) {
+                if constexpr (ROWS) store_row_piece<8>(X, grp, 256, dst, lane);
+                else store_native_piece<8>(X, grp, dst, lane);
+            }
             if (grp == 0 && msk) store_mask<8>(X, msk, lane);
         };
     };
@@ -188,7 +197,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
                                             if (!save) return;
                                             f32x4 v = {pe[4 * grp], pe[4 * grp + 1], pe[4 * grp + 2],
                                                        pe[4 * grp + 3]};
-                                            *reinterpret_cast<f32x4*>(pdst + (grp * 64 + lane) * 4) = v;
+                                            float* d = ROWS ? pdst + (lane & 31) * 64 + 32 * h + 4 * grp
+                                                            : pdst + (grp * 64 + lane) * 4;
+                                            *reinterpret_cast<f32x4*>(d) = v;
                                         });
         relu<8>(A);
     }
@@ -257,11 +268,11 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
         else pe_encode<6, NR_DIR_KSTEPS>(dpe, dx, dy, dz, h);
         f32x16 C[4];
         init_bias<4>(C, H + NR_H_BDIR, h);
-        float* fdst = SV + nr_sv_feat(nb) + (size_t)blk * NR_NATIVE(256);
+        // feat is not saved: the dir layer's feat-column weight gradient is
+        // formed from h8 (wgrad.hip task 10, nr_wgrad_dir_feat)
         const float* dpw = P + NR_F_DIR + NR_PL(128, 4);
         nr_mm_chain<128, 4, 4>(P + NR_F_DIR, dpw, lane, C, wq,
-                               [&](int g) { return A[g >> 4][g & 15]; },
-                               side_acc8(A, fdst, nullptr));
+                               [&](int g) { return A[g >> 4][g & 15]; });
         float* ddst = SV + nr_sv_dirpe(nb) + (size_t)blk * NR_NATIVE(32);
         nr_mm_chain<NR_DIR_KSTEPS, 4, 4>(dpw, nullptr, lane, C, wq,
                                          [&](int g) { return dpe[g]; },
@@ -269,7 +280,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
                                              if (!save) return;
                                              f32x4 v = {dpe[4 * grp], dpe[4 * grp + 1],
                                                         dpe[4 * grp + 2], dpe[4 * grp + 3]};
-                                             *reinterpret_cast<f32x4*>(ddst + (grp * 64 + lane) * 4) = v;
+                                             float* d = ROWS ? ddst + (lane & 31) * 32 + 16 * h + 4 * grp
+                                                             : ddst + (grp * 64 + lane) * 4;
+                                             *reinterpret_cast<f32x4*>(d) = v;
                                          });
         relu<4>(C);
 
@@ -285,7 +298,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd_kernel(FwdArgs a) {
             *reinterpret_cast<f32x4*>(a.out + (size_t)s * 4) = o;
         }
         if (save) {   // hdir: last layer, stored at the end
-            store_native<4>(C, SV + nr_sv_hdir(nb) + (size_t)blk * NR_NATIVE(128), lane);
+            float* hd = SV + nr_sv_hdir(nb) + (size_t)blk * NR_NATIVE(128);
+            if constexpr (ROWS) store_rows<4>(C, hd, lane);
+            else store_native<4>(C, hd, lane);
             store_mask<4>(C, mseg(8), lane);
         }
     }

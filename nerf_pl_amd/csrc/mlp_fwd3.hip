@@ -162,7 +162,8 @@ enum FwdMode { FWD_RAYS = 0, FWD_EMB = 1, FWD_PTS = 2 };
 // layer 1's side: the xyz PE slots saved, 2 float4 per group (tiles 2, 6)
 template <bool SAVE, bool ROWS>
 struct PeSide {
-    static constexpr int kBefore7 = SAVE ? 2 : 0;
+    // stores at tiles 2 and 6
+    static constexpr int before(int T) { return SAVE ? (T > 2) + (T > 6) : 0; }
     const float (&pe)[2][16];
     float* dst;
     int g, lane;
@@ -180,7 +181,8 @@ struct PeSide {
 // the dir layer's PE part: the dir PE slots saved N16 at tiles 1, 3, 5, 7
 template <bool SAVE>
 struct DirPeSide {
-    static constexpr int kBefore7 = SAVE ? 3 : 0;
+    // stores at the odd tiles
+    static constexpr int before(int T) { return SAVE ? T / 2 : 0; }
     const float (&dpe)[2][8];
     float* dst;
     int g, lane;
@@ -280,7 +282,8 @@ struct PeU {
 };
 
 // NR_X3_DBG 8 (dev timing build): per-layer clock stamps, 16 uint64 per wave
-// in the save pointer: [0] start realtime, [1] end realtime, [2] cycles,
+// in the out buffer (no outputs written; saving as asked): [0] start
+// realtime, [1] end realtime, [2] cycles,
 // [3 + i] cycles at stamp i (0 inputs+PE, 1 first hand-over, 2.. segments)
 #if NR_X3_DBG == 8
 #define NR_STAMP(i) (stamps[i] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0))
@@ -405,7 +408,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 #endif
     NR_STAMP(0);       // inputs + positional encoding
 
-    Frag f0;           // tile-0 fragments of the next k-group
+    Ahead f0;          // the first tiles' fragments of the next k-group
     enter<FwdTab, 0, QEND>(smem, lane, f0);
     NR_STAMP(1);       // prologue: + first weight group
 
@@ -525,8 +528,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 #endif
         PeU<8> dpeu{dpe};
         // xyz_encoding_final: no activation (nerf.py:116)
-        AccU<false, SAVE, false, false> uf{A, SV + nr_sv_feat(nb) + (size_t)blk * NR_SEGF(256),
-                                           nullptr, nullptr, lane, g};
+        // not saved: the weight gradient of the dir layer's feat columns is
+        // formed from h8 (wgrad.hip task 10, nr_wgrad_dir_feat) -- 1 KiB per
+        // sample fewer stores, and the densest store phase of the kernel gone
+        AccU<false, false, false, false> uf{A, nullptr, nullptr, nullptr, lane, g};
         { auto bi = bias(NR_H_BFINAL); segment<FwdTab, kFinal, 8, 2, QEND, true>(dma, lane, A, u8, uf, bi, none, b, f0); }
         NR_STAMP(11);
         float sigma[2];
@@ -547,7 +552,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         float zc[3][2];
 #pragma unroll
         for (int c = 0; c < 3; ++c) head_dot<true>(C, H + NR_H_WRGB + 128 * c, g, zc[c]);
-        if (wr && !LIST) {
+        if (wr && !LIST && NR_X3_DBG != 8) {
             f32x4 o;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -559,7 +564,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         }
 #if NR_X3_DBG == 8
         if (lane == 0) {
-            uint64_t* st = reinterpret_cast<uint64_t*>(a.save) + (size_t)blk * 16;
+            uint64_t* st = reinterpret_cast<uint64_t*>(a.out) + (size_t)blk * 16;
             st[0] = r0;
             st[1] = __builtin_amdgcn_s_memrealtime();
             st[2] = __builtin_amdgcn_s_memtime() - t0;
@@ -662,8 +667,7 @@ NR_API int NR_X3_NAME(nr_mlp_fwd)(const void* packed, const float* rays, const f
                samples_per_ray, xstride, out, save};
     const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
     hipStream_t st = (hipStream_t)stream;
-    // NR_X3_DBG 8 builds pass the clock-stamp buffer in save
-    const bool sv = save != nullptr && NR_X3_DBG != 8;
+    const bool sv = save != nullptr;
     if (emb) {
         if (sigma_only) mlp_fwd3_kernel<FWD_EMB, true, false><<<blocks, 64 * kWaves, 0, st>>>(a);
         else if (sv) mlp_fwd3_kernel<FWD_EMB, false, true><<<blocks, 64 * kWaves, 0, st>>>(a);

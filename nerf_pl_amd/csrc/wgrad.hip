@@ -15,6 +15,8 @@
 // gradient buffer in NeRF.named_parameters() order.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "x3.h"
 
 namespace {
@@ -162,16 +164,34 @@ struct SegGeo {
     }
 };
 
+// ROWS staging geometry of an input segment (sample-major rows of W): float4
+// e = tid + 512 i is chunk (e & 3) + 4 (e >> 7) of sample (e >> 2) & 31, so a
+// wave instruction reads 16 rows x 64 contiguous bytes (not 32 rows x 32 B)
+// while the [column][sample] image writes stay at most 2-way bank conflicted
+// (free for ds_write_b32); a thread's sample is the same in every iteration
+template <int KIND, int W>
+struct RowGeo {
+    static constexpr int F4 = W * 8;
+    static constexpr int ITERS = (F4 + kThreads - 1) / kThreads;
+    __device__ static __forceinline__ int j(int tid) { return (tid >> 2) & 31; }
+    __device__ static __forceinline__ int c(int tid, int i) {
+        return 4 * ((tid & 3) + 4 * ((tid + kThreads * i) >> 7));
+    }
+};
+
 // GAT: over the packed sample list (the fp32 *_active entry points): the
-// gradient operand is read by position, the input operand gathered -- the
-// float4 of column c of sample s sits at (s >> 5) * F4 + (e & ~31) + (s & 31) of
-// its block-native segment, so each thread resolves one sample per stage;
-// positions past m stage zeros
-template <int KA, int WA, int KB, int WB, int WM, int WN, bool GAT = false>
+// gradient operand is read by position, the input operand gathered, each
+// thread resolving one sample per stage; positions past m stage zeros.
+// ROWS: the input operand saved as sample-major rows (mlp_fwd.hip, the full
+// graph): the float4 of column c of sample s is row s at c -- a gathered
+// sample's 128-B lines are read whole, and the same thread -> (sample,
+// column) mapping keeps the LDS image writes conflict-free.  Else
+// block-native: the float4 sits at (s >> 5) * F4 + (e & ~31) + (s & 31).
+template <int KA, int WA, int KB, int WB, int WM, int WN, bool GAT = false, bool ROWS = false>
 __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int b0, int b1,
                                            float* lds, float* __restrict__ slab) {
     using GA = SegGeo<KA, WA>;
-    using GB = SegGeo<KB, WB>;
+    using GB = std::conditional_t<ROWS && KB != SEG_HEAD, RowGeo<KB, WB>, SegGeo<KB, WB>>;
     constexpr int MT = (WA / WM + 31) / 32, NT = (WB / WN + 31) / 32;
     constexpr int M = WA, N = WB;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -197,7 +217,16 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
     auto load = [&](int blk) {
         const f32x4* pa = reinterpret_cast<const f32x4*>(T.a.base) + (size_t)blk * GA::F4 + tid;
         const f32x4* pb;
-        if constexpr (GAT) {
+        if constexpr (ROWS) {
+            const int sj = GAT ? a.slist[min(blk * 32 + jb, m - 1)] : blk * 32 + jb;
+            const float* row = T.b.base + (size_t)sj * WB;
+#pragma unroll
+            for (int i = 0; i < GA::ITERS; ++i) if (ta) ra[i] = pa[kThreads * i];
+#pragma unroll
+            for (int i = 0; i < GB::ITERS; ++i)
+                if (tb) rb[i] = *reinterpret_cast<const f32x4*>(row + GB::c(tid, i));
+            return;
+        } else if constexpr (GAT) {
             const int sj = a.slist[min(blk * 32 + jb, m - 1)];
             pb = reinterpret_cast<const f32x4*>(T.b.base) + (size_t)(sj >> 5) * GB::F4 +
                  (tid - jb) + (sj & 31);
@@ -305,7 +334,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const WgTask& T, int
     }
 }
 
-template <bool GA>
+template <bool GA, bool ROWS>
 __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[2 * kBuf];   // 144 KiB
     int t = 0;
@@ -321,17 +350,17 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
     // (WM, WN) = wave grid over the task's output (<= 8 waves; 128 accumulators max)
     switch (__builtin_amdgcn_readfirstlane(T.id)) {
         case 0: case 4:
-            wgrad_body<SEG_ACC, 256, SEG_PE, 64, 8, 1, GA>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 256, SEG_PE, 64, 8, 1, GA, ROWS>(a, T, b0, b1, lds, slab); break;
         case 10:
-            wgrad_body<SEG_ACC, 128, SEG_ACC, 256, 2, 4, GA>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 128, SEG_ACC, 256, 2, 4, GA, ROWS>(a, T, b0, b1, lds, slab); break;
         case 11:
-            wgrad_body<SEG_ACC, 128, SEG_DPE, 32, 4, 1, GA>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 128, SEG_DPE, 32, 4, 1, GA, ROWS>(a, T, b0, b1, lds, slab); break;
         case 12:
-            wgrad_body<SEG_HEAD, 4, SEG_ACC, 256, 1, 8, GA>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_HEAD, 4, SEG_ACC, 256, 1, 8, GA, ROWS>(a, T, b0, b1, lds, slab); break;
         case 13:
-            wgrad_body<SEG_HEAD, 4, SEG_ACC, 128, 1, 4, GA>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_HEAD, 4, SEG_ACC, 128, 1, 4, GA, ROWS>(a, T, b0, b1, lds, slab); break;
         default:
-            wgrad_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4, GA>(a, T, b0, b1, lds, slab); break;
+            wgrad_body<SEG_ACC, 256, SEG_ACC, 256, 2, 4, GA, ROWS>(a, T, b0, b1, lds, slab); break;
     }
 }
 
@@ -356,6 +385,9 @@ __global__ void __launch_bounds__(kThreads, 2) wgrad_kernel(WgArgs a) {
 #endif
 #ifndef NR_W3_MULTI
 #define NR_W3_MULTI 1
+#endif
+#ifndef NR_W3_EARLY
+#define NR_W3_EARLY 0
 #endif
 // Cache policy of the saved-segment reads (each byte is read once).  The
 // bf16 LDS-DMA reads are non-temporal: fine-pass wgrad 1.447 -> 1.388 ms
@@ -676,7 +708,10 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
     // 4 columns) are spread between the row tiles' MFMAs so their VALU and
     // LDS-store work overlaps the MFMAs in flight instead of idling both waves
     // of a SIMD at the same time; the extra operand's 4 units follow its MFMAs
-    auto compute_store = [&](int buf, int set, int st_next) {
+    // NR_W3_EARLY: all store units first, then the reload of the freed set
+    // (after(): two compute phases of latency for the loads instead of one),
+    // then the MFMAs -- the partner wave of the SIMD covers the staging VALU
+    auto compute_store = [&](int buf, int set, int st_next, auto after) {
         const int nval = st_next < nst ? m - (b0 + (st_next >> 1)) * 32 - 16 * (st_next & 1) : 0;
         char* ia = lds + (buf ^ 1) * kBufB;
         char* ib = ia + kOpnd;
@@ -692,6 +727,12 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
         const char* la = cur + (m0 + col) * kColB + 16 * h;
         const char* lb = cur + kOpnd + (n0 + col) * kColB + 16 * h;
         const bool go = (WM * WN == 8 || active) && NR_W3_DBG != 1;
+        if constexpr (NR_W3_EARLY) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) unit(u);
+            if constexpr (HX) if (NR_W3_DBG != 3) sx[set].store(ix, nval, xbacc[0], xbacc[1], scx);
+            after();
+        }
         x3::Pieces bp[NT];
         if (go) {
 #pragma unroll
@@ -712,9 +753,11 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
                 for (int j = 0; j < NT; ++j) acc[i][j] = x3::mfma_xp(ap, bp[j], acc[i][j]);
 #endif
             }
+            if constexpr (!NR_W3_EARLY) {
 #pragma unroll
-            for (int v = 0; v < UPT; ++v)
-                if (i * UPT + v < 8) unit(i * UPT + v);
+                for (int v = 0; v < UPT; ++v)
+                    if (i * UPT + v < 8) unit(i * UPT + v);
+            }
         }
         if constexpr (HX) {
             // extra output: A rows from the A image (XS = 0) or the X image,
@@ -733,12 +776,12 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
                     ap[k] = *reinterpret_cast<const x3::p8*>(xa + 32 * i * kColB + k * PA);
                 x3::mfma_xp_multi<XNT>(ap, xp, xacc[i]);
             }
-            if (NR_W3_DBG != 3) sx[set].store(ix, nval, xbacc[0], xbacc[1], scx);
+            if constexpr (!NR_W3_EARLY) if (NR_W3_DBG != 3) sx[set].store(ix, nval, xbacc[0], xbacc[1], scx);
         }
 #if NR_W3_SGB
         // interleave: per row tile, its fragment reads, then each MFMA followed
         // by two VALU ops of the store units, then the units' LDS stores
-        if constexpr (WM * WN == 8) {
+        if constexpr (WM * WN == 8 && !NR_W3_EARLY) {
             __builtin_amdgcn_sched_group_barrier(0x100, x3::kNP * NT, 0);
 #pragma unroll
             for (int i = 0; i < MT; ++i) {
@@ -761,6 +804,7 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
             }
         }
 #endif
+        if constexpr (!NR_W3_EARLY) after();
     };
     // stage st lives in LDS buffer st & 1 and register set st & 1; a set is
     // reloaded (two stages ahead) as soon as its stage has been stored
@@ -771,11 +815,11 @@ __device__ __forceinline__ void wgrad3_body(const WgArgs& a, const WgTask& T, in
     barrier();
 #pragma unroll 1
     for (int st = 0; st < nst; st += 2) {
-        compute_store(0, 1, st + 1);  // stage st from buffer 0; set 1 (stage st+1) -> buffer 1
-        load(1, st + 3);
+        // stage st from buffer 0; set 1 (stage st+1) -> buffer 1, then set 1 reloaded
+        compute_store(0, 1, st + 1, [&] { load(1, st + 3); });
         barrier();
-        compute_store(1, 0, st + 2);  // stage st+1 from buffer 1; set 0 (stage st+2) -> buffer 0
-        load(0, st + 4);
+        // stage st+1 from buffer 1; set 0 (stage st+2) -> buffer 0, then set 0 reloaded
+        compute_store(1, 0, st + 2, [&] { load(0, st + 4); });
         barrier();
     }
     // bias sums: reduce the 8 sample pairs of each (chunk, half) group of the
@@ -1285,6 +1329,34 @@ __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
 }  // namespace
 
 #if NR_X3_BASE_OBJECT
+// dir_encoding.0.weight's first 256 columns (the xyz_encoding_final input,
+// nerf.py:118): the weight-gradient launch leaves G = sum_s dz_dir h8^T there
+// (task 10); the gradient of the reference's dW = sum_s dz_dir feat^T with
+// feat = W_final h8 + b_final is G W_final^T + db_dir b_final^T.  One
+// workgroup per output row (in place: a row reads only itself), fp32 fma
+// chains over k in order.
+__global__ void __launch_bounds__(256) dir_feat_kernel(const float* __restrict__ params,
+                                                       float* __restrict__ grad) {
+    __shared__ float g[256];
+    const int o = blockIdx.x, c = threadIdx.x;
+    constexpr int kFan = 283;                       // dir_encoding.0 fan-in
+    float* row = grad + kP.w[9] + o * kFan;
+    g[c] = row[c];
+    __syncthreads();
+    const float* w = params + kP.w[8] + c * 256;    // xyz_encoding_final.weight row c
+    float acc = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 256; ++k) acc = fmaf(g[k], w[k], acc);
+    row[c] = fmaf(grad[kP.b[9] + o], params[kP.b[8] + c], acc);
+}
+
+NR_API int nr_wgrad_dir_feat(const float* params, float* grad_flat, void* stream) {
+    NR_REQUIRE(params && grad_flat, "nr_wgrad_dir_feat: null pointer");
+    dir_feat_kernel<<<128, 256, 0, (hipStream_t)stream>>>(params, grad_flat);
+    NR_LAUNCH_CHECK("nr_wgrad_dir_feat");
+    return 0;
+}
+
 NR_API int64_t nr_wgrad_workspace_bytes(int64_t n) {
     (void)n;
     // upper bound of sum_t G_t * (M_t N_t + M_t) for the task list below
@@ -1320,13 +1392,17 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     const WgSeg head{GD + nr_gd_dhead(nbp), SEG_HEAD, 4};
     auto H = [&](int l) { return acc(SV + nr_sv_h(l, nbp), 256); };
     auto DZ = [&](int l) { return acc(GD + nr_gd_dz(l, nbp), 256); };
-    const WgSeg feat = acc(SV + nr_sv_feat(nbp), 256), hdir = acc(SV + nr_sv_hdir(nbp), 128);
+    // task 10 (dir_encoding's feat columns) reads h8, not xyz_encoding_final's
+    // output: dW = sum dz_dir feat^T = G W_final^T + db_dir b_final^T with
+    // G = sum dz_dir h8^T (nerf.py:116, feat = W_final h8 + b_final), so the
+    // forward saves no feat; nr_wgrad_dir_feat finishes it
+    const WgSeg hdir = acc(SV + nr_sv_hdir(nbp), 128);
     const WgSeg dzdir = acc(GD + nr_gd_dzdir(nbp), 128);
     // (a, b, wm, wn); task order fixes wgrad_dest / wgrad_bias_dest
     const WgTask tasks[kTasks] = {
         {DZ(0), pe, 8, 1}, {DZ(1), H(0), 2, 4}, {DZ(2), H(1), 2, 4}, {DZ(3), H(2), 2, 4},
         {DZ(4), pe, 8, 1}, {DZ(4), H(3), 2, 4}, {DZ(5), H(4), 2, 4}, {DZ(6), H(5), 2, 4},
-        {DZ(7), H(6), 2, 4}, {DZ(8), H(7), 2, 4}, {dzdir, feat, 2, 4}, {dzdir, dpe, 4, 1},
+        {DZ(7), H(6), 2, 4}, {DZ(8), H(7), 2, 4}, {dzdir, H(7), 2, 4}, {dzdir, dpe, 4, 1},
         {head, H(7), 1, 8}, {head, hdir, 1, 4},
     };
     WgArgs a{};
@@ -1437,8 +1513,12 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     else if (x3 && slist && gather) wgrad3_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else if (x3 && !sigma_only) wgrad3_kernel<false, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else if (x3) wgrad3_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
-    else if (slist && gather) wgrad_kernel<true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
-    else wgrad_kernel<false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    // the full graph's inputs are sample-major rows (mlp_fwd.hip ROWS), the
+    // sigma-only graph's block-native
+    else if (slist && gather && !sigma_only && NR_F32_ROWS) wgrad_kernel<true, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (slist && gather) wgrad_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else if (!sigma_only && NR_F32_ROWS) wgrad_kernel<false, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    else wgrad_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
 #endif
     NR_LAUNCH_CHECK("nr_wgrad");
     dim3 rg((256 * 256 + 256 + 255) / 256, kTasks);

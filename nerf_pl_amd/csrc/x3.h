@@ -345,6 +345,17 @@ __device__ __forceinline__ void rd_frag(char* ring, int lane, int t, Frag& f) {
     for (int k = 0; k < kNP; ++k) f.p[k] = *reinterpret_cast<const p8*>(s + k * kTiles * 1024);
 }
 
+// LDS fragment lookahead in tiles: the weight fragments of tile t + kPF are
+// read while tile t multiplies (NR_X3_PF = 2 hands the next group over one
+// tile earlier and keeps a third fragment set, 8 more VGPRs)
+#ifndef NR_X3_PF
+#define NR_X3_PF 1
+#endif
+constexpr int kPF = NR_X3_PF;
+static_assert(kPF >= 1 && kPF <= 2, "fragment lookahead of 1 or 2 tiles");
+// the fragments of the next group's first kPF tiles, carried between groups
+struct Ahead { Frag f[kPF]; };
+
 // hand group Q over (wait + barrier) and read its tile-0 fragments; in the
 // merged ring a group that shares its predecessor's super-group arrived with
 // it, and only its tile-0 fragments are read
@@ -355,6 +366,11 @@ __device__ __forceinline__ void enter(char* ring, int lane, Frag& f0) {
             ring_enter<TAB, Q, QEND, EXTRA>();
         rd_frag<TAB, Q>(ring, lane, 0, f0);
     }
+}
+template <class TAB, int Q, int QEND, int EXTRA = 0>
+__device__ __forceinline__ void enter(char* ring, int lane, Ahead& a) {
+    enter<TAB, Q, QEND, EXTRA>(ring, lane, a.f[0]);
+    if constexpr (Q < QEND && kPF > 1) rd_frag<TAB, Q>(ring, lane, 1, a.f[1]);
 }
 
 __device__ __forceinline__ f32x4 mfma16(const p8& a, const p8& b, f32x4 c) {
@@ -405,32 +421,37 @@ struct BiasInit {     // bias[16F + 4g .. +3] (LDS), the same for both sample ti
 };
 
 // one k-group: acc[F0 + t][S] (+)= W_q[t] * B[S] for the 8 output tiles; with
-// INIT the k-group starts from cinit(F, S) instead of acc.  On entry f0
-// holds tile 0 of group Q; the fragments of tile t+1 are read while tile t
-// multiplies, and the hand-over of group Q+1 (wait, barrier, its tile-0 read)
-// is done before the last tile's MFMAs, so both the barrier and the first LDS
-// latency of the next group hide under MFMAs in flight.  On exit f0 holds
-// tile 0 of group Q+1.  hook(t) runs inside tile t; its VALU work is
-// interleaved with the tile's 2 kNProd MFMAs.
+// INIT the k-group starts from cinit(F, S) instead of acc.  On entry a holds
+// tiles 0 .. kPF-1 of group Q; the fragments of tile t+kPF are read while tile
+// t multiplies, and the hand-over of group Q+1 (wait, barrier, its tile-0
+// read) is done before the MFMAs of tile 8 - kPF, so both the barrier and the
+// first LDS latency of the next group hide under MFMAs in flight.  On exit a
+// holds tiles 0 .. kPF-1 of group Q+1.  hook(t) runs inside tile t; its VALU
+// work is interleaved with the tile's 2 kNProd MFMAs.  EXTRA: the stores the
+// hooks issue before the hand-over tile (left in flight by its vmcnt wait).
 template <class TAB, int Q, int QEND, int F0, bool INIT, int EXTRA, typename CInit, typename Hook, int NF>
 __device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][2],
-                                         const Pieces (&b)[2], CInit& cinit, Hook& hook, Frag& f0) {
-    Frag f[2];
-    f[0] = f0;
+                                         const Pieces (&b)[2], CInit& cinit, Hook& hook, Ahead& a) {
+    constexpr int NR = kPF + 1;       // fragment sets in registers
+    Frag f[NR];
+#pragma unroll
+    for (int i = 0; i < kPF; ++i) f[i] = a.f[i];
     f32x4 ci[2][2];
     if constexpr (INIT) { ci[0][0] = cinit(F0, 0); ci[0][1] = cinit(F0, 1); }
 #pragma unroll
     for (int t = 0; t < kTiles; ++t) {
-        if (t + 1 < kTiles) {
-            rd_frag<TAB, Q>(ring, lane, t + 1, f[(t + 1) & 1]);
-            if constexpr (INIT) { ci[(t + 1) & 1][0] = cinit(F0 + t + 1, 0); ci[(t + 1) & 1][1] = cinit(F0 + t + 1, 1); }
+        const int tn = t + kPF;
+        if (tn < kTiles) rd_frag<TAB, Q>(ring, lane, tn, f[tn % NR]);
+        else if (tn == kTiles) enter<TAB, Q + 1, QEND, EXTRA>(ring, lane, a.f[0]);
+        else if constexpr (Q + 1 < QEND) rd_frag<TAB, Q + 1>(ring, lane, tn - kTiles, a.f[tn - kTiles]);
+        if constexpr (INIT) {
+            if (t + 1 < kTiles) { ci[(t + 1) & 1][0] = cinit(F0 + t + 1, 0); ci[(t + 1) & 1][1] = cinit(F0 + t + 1, 1); }
         }
-        if (t == kTiles - 1) enter<TAB, Q + 1, QEND, EXTRA>(ring, lane, f0);
         __builtin_amdgcn_sched_barrier(0);
         f32x4& d0 = acc[F0 + t][0];
         f32x4& d1 = acc[F0 + t][1];
-        if constexpr (INIT) x6_pair(f[t & 1], b, ci[t & 1][0], ci[t & 1][1], d0, d1);
-        else x6_pair(f[t & 1], b, d0, d1, d0, d1);
+        if constexpr (INIT) x6_pair(f[t % NR], b, ci[t & 1][0], ci[t & 1][1], d0, d1);
+        else x6_pair(f[t % NR], b, d0, d1, d0, d1);
         // keep the tile's MFMAs in this tile: MFMA intrinsics have no side
         // effects, so without an ordered use the instruction selector may
         // float them anywhere in the (huge) basic block
@@ -458,9 +479,9 @@ __device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][
 //   side(IC<G>, t): side work at tile t of group G (output stores)
 // The 8 split units (S, p) of the next k-step run one per tile of the last
 // half's group; one DMA instruction of group Q+3 runs per tile 0..5.
-//   Getters declare kStores (a global store per odd unit), sides kBefore7,
-//   the stores they issue in a group before its tile 7 (where the next
-//   group's DMA is waited for).
+//   Getters declare kStores (a global store per odd unit), sides before(T),
+//   the stores they issue in a group before its tile T (the hand-over tile,
+//   where the next group's DMA is waited for).
 // Getters also have begin(producer): called before their first unit once the
 // getter that fed this layer (the producer) has split all of its units.
 struct NoNext {
@@ -475,7 +496,7 @@ template <typename T> struct IsNoNext { static constexpr bool value = false; };
 template <> struct IsNoNext<NoNext> { static constexpr bool value = true; };
 
 struct NoSide {
-    static constexpr int kBefore7 = 0;
+    static constexpr int before(int) { return 0; }
     template <typename T> __device__ __forceinline__ void operator()(T, int) const {}
 };
 
@@ -509,13 +530,15 @@ __host__ __device__ constexpr int unit_at(int t) {
     if constexpr (NH == 1) return t;
     else return t >= 3 && t <= 6 ? 4 * HF + t - 3 : -1;
 }
-// stores a storing getter issues before tile 7 of its group: one per odd unit,
-// or (PAIRED: the two halves of a 128-B row line together, x3.h store_row_pair)
-// two per unit p = 3
+// the tile whose start hands the next group over (x3.h group_mm)
+constexpr int kHandTile = kTiles - kPF;
+// stores a storing getter issues before the hand-over tile of its group: one
+// per odd unit, or (PAIRED: the two halves of a 128-B row line together, x3.h
+// store_row_pair) two per unit p = 3
 template <int NH, int HF, bool PAIRED = false>
-__host__ __device__ constexpr int stores_before7() {
+__host__ __device__ constexpr int stores_before_hand() {
     int n = 0;
-    for (int t = 0; t < kTiles - 1; ++t) {
+    for (int t = 0; t < kHandTile; ++t) {
         const int u = unit_at<NH, HF>(t);
         if (u < 0) continue;
         if (PAIRED) n += (u & 3) == 3 ? 2 : 0;
@@ -528,7 +551,7 @@ template <class TAB, int Q0, int S, int KS, int NH, int QEND, bool INIT, int HF,
           typename NextU, typename CInit, typename Side, int NF>
 __device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)[NF][2], GetU& getu,
                                           NextU& nextu, CInit& cinit, Side& side,
-                                          const Pieces (&b)[2], Pieces (&bn)[2], Frag& f0) {
+                                          const Pieces (&b)[2], Pieces (&bn)[2], Ahead& f0) {
     if constexpr (HF < NH) {
         constexpr int Q = Q0 + NH * S + HF;
         auto hook = [&](int t) {
@@ -545,7 +568,7 @@ __device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)
         };
         constexpr bool ust = S + 1 < KS ? GetU::kStores : NextU::kStores;
         constexpr bool upr = S + 1 < KS ? GetU::kPaired : NextU::kPaired;
-        constexpr int extra = (ust ? stores_before7<NH, HF, upr>() : 0) + Side::kBefore7;
+        constexpr int extra = (ust ? stores_before_hand<NH, HF, upr>() : 0) + Side::before(kHandTile);
         group_mm<TAB, Q, QEND, 8 * HF, INIT && S == 0, extra>(dma.ring, lane, acc, b, cinit, hook, f0);
         seg_group<TAB, Q0, S, KS, NH, QEND, INIT, HF + 1>(dma, lane, acc, getu, nextu, cinit, side,
                                                           b, bn, f0);
@@ -556,7 +579,7 @@ template <class TAB, int Q0, int S, int KS, int NH, int QEND, bool INIT, typenam
           typename NextU, typename CInit, typename Side, int NF>
 __device__ __forceinline__ void seg_from(const Dma& dma, int lane, f32x4 (&acc)[NF][2], GetU& getu,
                                          NextU& nextu, CInit& cinit, Side& side,
-                                         Pieces (&b)[2], Frag& f0) {
+                                         Pieces (&b)[2], Ahead& f0) {
     if constexpr (S < KS) {
         Pieces bn[2];
         seg_group<TAB, Q0, S, KS, NH, QEND, INIT, 0>(dma, lane, acc, getu, nextu, cinit, side, b, bn, f0);
@@ -572,7 +595,7 @@ template <class TAB, int Q0, int KS, int NH, int QEND, bool INIT, typename GetU,
           typename CInit, typename Side, int NF>
 __device__ __forceinline__ void segment(const Dma& dma, int lane, f32x4 (&acc)[NF][2], GetU& getu,
                                         NextU& nextu, CInit& cinit, Side& side, Pieces (&b)[2],
-                                        Frag& f0) {
+                                        Ahead& f0) {
     seg_from<TAB, Q0, 0, KS, NH, QEND, INIT>(dma, lane, acc, getu, nextu, cinit, side, b, f0);
 }
 

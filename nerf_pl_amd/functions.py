@@ -169,6 +169,9 @@ class _FusedMLP(torch.autograd.Function):
                 ctx.save_for_backward(out, save, packed_f, packed_b)
             ctx.defer = defer
             ctx.sigma_only = sigma_only
+            # the flat parameters the forward ran with (the dir layer's
+            # feat-column weight gradient needs W_final, b_final: nr_wgrad_dir_feat)
+            ctx.flat = model.flat_params()
             ctx.model = model if DEFER_SAVE == "auto" else None
             ctx.so_kernels = so_train
         if sigma_only and train and out.shape[1] == 4:
@@ -209,6 +212,8 @@ class _FusedMLP(torch.autograd.Function):
         ws = _wgrad_workspace(dev.index, int(st))
         call(ops.entry("nr_wgrad" + sfx, packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
              ws.data_ptr(), gflat.data_ptr(), *active, st)
+        if not ctx.so_kernels:
+            _dir_feat(ctx, gflat, st)
         if _DEBUG is not None:
             _DEBUG.update(save=save, grad_ws=grad_ws, g_out=g_out, gflat=gflat, n=n)
             _DEBUG.setdefault("g_outs", []).append(g_out)
@@ -250,7 +255,15 @@ class _FusedMLP(torch.autograd.Function):
         ws = _wgrad_workspace(dev.index, int(st))
         call(ops.entry("nr_wgrad" + sfx, packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
              ws.data_ptr(), gflat.data_ptr(), *lst, st)
+        if not so:
+            _dir_feat(ctx, gflat, st)
         return (None,) * 6 + _param_grads(gflat, ctx.sigma_only)
+
+
+def _dir_feat(ctx, gflat, st):
+    """dir_encoding.0.weight's feat columns: the weight-gradient launch leaves
+    G = sum dz_dir h8^T there (feat is not saved); G W_final^T + db b_final^T"""
+    call("nr_wgrad_dir_feat", ctx.flat.data_ptr(), gflat.data_ptr(), st)
 
 
 def _param_grads(gflat, sigma_only):

@@ -314,19 +314,12 @@ def n16_to_rows(seg: torch.Tensor, n: int, width: int) -> torch.Tensor:
 
 
 def saved_rows(seg: torch.Tensor, n: int, width: int) -> torch.Tensor:
-    """An activation segment of the split arithmetics' training forward
-    (csrc/x3.h store_row): sample-major rows of ``width`` values (PE segments:
-    columns are PE slots, packing.PE16_MAP / DIR16_MAP) -> (n, width)."""
+    """An activation segment of a full-graph training forward (csrc/x3.h
+    store_row; exact fp32: layout.h store_row_piece): sample-major rows of
+    ``width`` values (PE segments: columns are PE slots, packing.PE16_MAP /
+    DIR16_MAP, or for fp32 the packed k order 32h + g / 16h + g) -> (n, width)."""
     nb = n_blocks(n)
     return seg[: nb * BLK * width].view(nb * BLK, width)[:n]
-
-
-def pe_to_rows(seg: torch.Tensor, n: int, ksteps: int) -> torch.Tensor:
-    """Decode a PE segment [block][g/4][lane][g%4] to (n, 2*ksteps) rows with
-    column 32h+g (xyz, ksteps=32) / 16h+g (dir, ksteps=16) = pe value (g, h)."""
-    nb = n_blocks(n)
-    x = seg[: nb * BLK * 2 * ksteps].view(nb, ksteps // 4, 2, BLK, 4)
-    return x.permute(0, 3, 2, 1, 4).reshape(nb * BLK, 2 * ksteps)[:n]
 
 
 def save_segments(sv: torch.Tensor, n: int) -> dict:

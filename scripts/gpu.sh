@@ -82,7 +82,7 @@ for step in "$@"; do
         esac
         name=ab_$(echo "$v" | tr ':=/' '___')_$i
         run "$name" 200 env "${envs[@]}" python bench.py --fp32-leg-steps 0 --cpu-baseline-seconds 0 ${BENCH_ARGS:-}
-        grep -h '^{' "$out/$name.log" | python -c 'import json,sys; j=json.loads(sys.stdin.read()); r=j["rooflines"]; print(j["value"], j["ms_per_step"], *[(k, r[k]["avg_launch_ms"]) for k in r])' || true
+        grep -h '^{' "$out/$name.log" | python -c 'import json,sys; j=json.loads(sys.stdin.read()); r=j["rooflines"]; f=j.get("fp32_leg") or {}; print(j["value"], j["ms_per_step"], *[(k, r[k]["avg_launch_ms"]) for k in r], "| fp32 leg", f.get("value"), *[(k, v["avg_launch_ms"]) for k, v in (f.get("rooflines") or {}).items()])' || true
       done
     done ;;
   dist)

@@ -28,6 +28,8 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     flat = (torch.rand(packing.N_PARAMS, device=dev) - 0.5) * 0.15
+    if os.environ.get("NR_KB_ZERO") == "1":     # all-zero weights: the power (DVFS) control
+        flat.zero_()
     pf, pb = ops.pack_fwd_fp32(flat), ops.pack_bwd_fp32(flat)
     p3, pb3 = ops.pack_fwd3(flat), ops.pack_bwd(flat, math="bf16x6")
     ph3, pbh3 = ops.pack_fwd3(flat, math="f16x3"), ops.pack_bwd(flat, math="f16x3")

@@ -53,6 +53,7 @@ def _cases():
             c += [(f"nr_pack{sfx}", [N, N, -1, N, N, N], NR_EINVAL),
                   (f"nr_pack_bwd{sfx}", [N, N, -1, N, N], NR_EINVAL)]
     c += [
+        ("nr_wgrad_dir_feat", [N, N, N], NR_EINVAL),
         ("nr_active_samples", [N, -1, N, N, N, N], NR_EINVAL),
         ("nr_active_samples", [N, 5, N, N, N, N], NR_EINVAL),
         ("nr_pack", [N, N, -1, N, N], NR_EINVAL),

@@ -142,6 +142,29 @@ class _LinBF16(torch.autograd.Function):
         return dx, rb(dy).T @ rb(x), db, None, None
 
 
+class _DirBF16(torch.autograd.Function):
+    """dir_encoding (nerf.py:118-119) as the kernels form its gradient: forward
+    and data gradient as _LinBF16 on cat[feat, dir PE]; the weight gradient of
+    the feat columns from h8 -- (rb(dy)^T rb(h8)) W_final^T + db b_final^T
+    (feat = W_final h8 + b_final is not saved, wgrad.hip task 10 +
+    nr_wgrad_dir_feat) -- and of the dir PE columns rb(dy)^T rb(x)."""
+
+    @staticmethod
+    def forward(ctx, feat, xd, h8, w, b, wf, bf):
+        x = torch.cat([feat, xd], -1)
+        ctx.save_for_backward(x, h8, w, wf, bf)
+        return rb(x) @ rb(w).T + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, h8, w, wf, bf = ctx.saved_tensors
+        dx = rb(dy) @ rb(w)
+        db = rb(dy).sum(0)
+        dw = rb(dy).T @ rb(x)
+        dw[:, :256] = (rb(dy).T @ rb(h8)) @ wf.T + db[:, None] * bf[None, :]
+        return dx[:, :256], None, None, dw, db, None, None
+
+
 def nerf_bf16_autograd(P, x):
     """Oracle MLP (nerf.py:83-124) on _LinBF16 layers: forward and backward
     with exactly the bf16 kernels' roundings."""
@@ -155,7 +178,9 @@ def nerf_bf16_autograd(P, x):
         h = torch.relu(L(h, f"xyz_encoding_{i + 1}.0"))
     sigma = L(h, "sigma", False, False)
     feat = L(h, "xyz_encoding_final")
-    hd = torch.relu(L(torch.cat([feat, xd], -1), "dir_encoding.0"))
+    hd = torch.relu(_DirBF16.apply(feat, xd, h, P["dir_encoding.0.weight"], P["dir_encoding.0.bias"],
+                                   P["xyz_encoding_final.weight"].detach(),
+                                   P["xyz_encoding_final.bias"].detach()))
     rgb = torch.sigmoid(L(hd, "rgb.0", False, False))
     return torch.cat([rgb, sigma], -1)
 

@@ -18,8 +18,9 @@ summation order -- so the oracle's own fp32 result sits up to 5e-3 of a
 tensor's norm from float64 (median ~7e-4).  The bound (tests/grad64.py):
 every tensor within max(1e-4, 2 x that fp32 distance) of float64, normwise,
 the fp32 distance the largest at the weights and at two points one fp32 ulp
-away, with the rays whose importance samples differ (bin flips, here or in
-float64) out of the functional.
+away, every evaluation's fine pass at our importance depths (which the
+reference detaches, rendering.py:253-255), and the rays whose compositing ReLU
+switched between ours and float64 out of the functional.
 """
 import numpy as np
 import pytest
@@ -69,7 +70,7 @@ def _draws(c):
     return d
 
 
-def _run(c, grad=False):
+def _run(c, grad=False, want_cap=False):
     from nerf_pl_amd import Embedding, NeRF, ReplayRNG, render_rays
     params = [O.make_params(21 + c["seed"] % 5, sigma_bias=0.5),
               O.make_params(22 + c["seed"] % 5, sigma_bias=0.5)]
@@ -100,7 +101,7 @@ def _run(c, grad=False):
         moved, explained = pdf_flips(cap["z_fine"], ocap, draws[-3])
         assert not (bad & ~moved).any(), f"z_fine differs without a moved importance depth, {c}"
         assert not (moved & ~explained).any(), f"z_fine moved away from any CDF knot, {c}"
-    return models, params, res, ref, bad
+    return (models, params, res, ref, bad, cap) if want_cap else (models, params, res, ref, bad)
 
 
 CASES = list(range(24))
@@ -127,9 +128,9 @@ def test_random_config_matches_oracle(seed, math, monkeypatch):
         assert ok.all(), f"{k}: max err {err[~bad].max():.3g} on {int((~ok).sum())} rays, {c}"
 
 
-def _oracle_grads(c, rays, draws, dt, ulp=None):
+def _oracle_grads(c, rays, draws, dt, ulp=None, z_fine=None):
     """the case's NeRF pair (optionally one fp32 ulp away, tests/grad64.py)
-    through the oracle in dtype dt"""
+    through the oracle in dtype dt, the fine pass at depths z_fine when given"""
     params = []
     for s in (21 + c["seed"] % 5, 22 + c["seed"] % 5):
         p = O.make_params(s, sigma_bias=0.5)
@@ -138,7 +139,7 @@ def _oracle_grads(c, rays, draws, dt, ulp=None):
     cap = {}
     args = (c["S"], c["use_disp"], c["perturb"], c["noise"], c["I"], 32768, c["white_back"], False)
     ref = O.render_rays(params, rays.to(dt), *args, rng=O.ReplayRNG([d.to(dt) for d in draws]),
-                        capture=cap)
+                        capture=cap, z_fine_override=z_fine)
     return params, ref, cap
 
 
@@ -151,11 +152,22 @@ def _functional(out, keep, seed):
     return tot
 
 
-def _zflips(c, cap32, cap64):
-    if c["I"] == 0:
-        return np.zeros(c["n"], bool)
-    z32, z64 = cap32["z_fine"].detach().double(), cap64["z_fine"].detach()
-    return ((z32 - z64).abs().max(1).values > 1e-4 * z64.abs().max(1).values.clamp(min=1)).numpy()
+def _kinks(c, models, rays, draws, cap, cap64):
+    """rays with a ReLU kink of the compositing between our sigma and the
+    float64 oracle's (tests/grad64.py relu_kinks), coarse and fine"""
+    from nerf_pl_amd import functions
+    S, I, r = c["S"], c["I"], rays.to(DEV)
+    passes = [(0, cap["z_coarse"], "raw_coarse", S, draws[1 if c["perturb"] > 0 else 0])]
+    if I > 0:
+        passes.append((1, cap["z_fine"], "raw_fine", S + I, draws[-1]))
+    out = np.zeros(c["n"], bool)
+    for mi, z, key, spr, noise in passes:
+        with torch.no_grad():
+            sig = functions.mlp_apply(models[mi], rays=r, z=z, spr=spr)[:, 3].view(-1, spr)
+        k, e = grad64.relu_kinks(sig, cap64[key][..., 3].reshape(-1, spr), noise * c["noise"])
+        assert e.all(), f"a compositing ReLU switched away from its kink, {c}"
+        out |= k
+    return out
 
 
 def _named(models_or_params, zeros_like=None):
@@ -179,19 +191,21 @@ def test_random_config_gradients_match_oracle(seed, math, monkeypatch):
     c = _config(seed)
     c["test_time"] = False
     c["n"] = max(c["n"], 64)
-    models, _, res, _, bad = _run(c, grad=True)
+    models, _, res, _, _, cap_ours = _run(c, grad=True, want_cap=True)   # asserts the forward
     rays, draws = _rays(c), _draws(c)
-    pts = {u: (_oracle_grads(c, rays, draws, torch.float32, u), _oracle_grads(c, rays, draws, torch.float64, u))
-           for u in (None, 1, 2)}
-    (_, _, cap32), (_, _, cap64) = pts[None]
-    bad = bad | _zflips(c, cap32, cap64)   # importance samples that differ in float64 are screened too
+    # every evaluation's fine pass at our depths (the reference detaches them,
+    # rendering.py:253-255; see test_gpu_cfg4.py)
+    zf = cap_ours["z_fine"].detach().cpu() if c["I"] > 0 else None
+    pts = {u: (_oracle_grads(c, rays, draws, torch.float32, u, zf),
+               _oracle_grads(c, rays, draws, torch.float64, u, zf)) for u in (None, 1, 2)}
+    (_, _, cap64) = pts[None][1]
+    # rays whose compositing ReLU switched between ours and float64 are screened
+    bad = _kinks(c, models, rays, draws, cap_ours, cap64)
     keep = torch.from_numpy(~bad)
     assert bad.sum() <= max(1, 0.05 * c["n"]), f"{bad.sum()} rays screened, {c}"
     _functional(res, keep, seed).backward()
     g32s, g64s = [], []
     for u, ((p32, r32, k32), (p64, r64, k64)) in pts.items():
-        if (_zflips(c, k32, k64) & ~bad).any():
-            continue            # a bin flip only at this ulp point: not a floor sample
         _functional(r32, keep, seed).backward()
         _functional(r64, keep, seed).backward()
         g32s.append(_named(p32))
