@@ -56,19 +56,11 @@
 // of branching around their stores (ops.n_blocks)
 __host__ __device__ __forceinline__ int64_t nr_blocks_pad(int64_t n) { return ((n + 127) / 128) * 4; }
 #define NR_MASK_LAYERS 9          // h1..h8, hdir
-#define NR_SAVE_PER_BLOCK (NR_NATIVE(64) + 8 * NR_NATIVE(256) + NR_NATIVE(256) + \
-                           NR_NATIVE(128) + NR_NATIVE(32) + NR_MASK_LAYERS * 256)
-struct NrSave {
-    float* pe; float* h[8]; float* feat; float* hdir; float* dirpe; uint32_t* mask;
-    __host__ __device__ NrSave(float* base, int64_t nb) {
-        pe = base;
-        for (int l = 0; l < 8; ++l) h[l] = base + NR_NATIVE(64) * nb + (int64_t)l * NR_NATIVE(256) * nb;
-        feat = base + (NR_NATIVE(64) + 8 * NR_NATIVE(256)) * nb;
-        hdir = feat + NR_NATIVE(256) * nb;
-        dirpe = hdir + NR_NATIVE(128) * nb;
-        mask = reinterpret_cast<uint32_t*>(dirpe + NR_NATIVE(32) * nb);
-    }
-};
+// PE, h1..h8, hdir, dir PE, masks.  xyz_encoding_final's output (feat) is
+// not saved: the weight gradient forms the dir layer's feat columns from h8
+// (wgrad.hip task 10, nr_wgrad_dir_feat)
+#define NR_SAVE_PER_BLOCK (NR_NATIVE(64) + 8 * NR_NATIVE(256) + NR_NATIVE(128) + NR_NATIVE(32) + \
+                           NR_MASK_LAYERS * 256)
 
 //   dz1..dz8, dfeat (256 wide), dzdir (128), dhead [block][j][4] = (dz_rgb, dsigma)
 #define NR_GRAD_PER_BLOCK (9 * NR_NATIVE(256) + NR_NATIVE(128) + NR_BLK * 4)
@@ -95,8 +87,7 @@ __host__ __device__ __forceinline__ int64_t nr_sv_pe(int64_t) { return 0; }
 __host__ __device__ __forceinline__ int64_t nr_sv_h(int l, int64_t nb) {
     return (NR_NATIVE(64) + (int64_t)l * NR_NATIVE(256)) * nb;
 }
-__host__ __device__ __forceinline__ int64_t nr_sv_feat(int64_t nb) { return nr_sv_h(8, nb); }
-__host__ __device__ __forceinline__ int64_t nr_sv_hdir(int64_t nb) { return nr_sv_h(9, nb); }
+__host__ __device__ __forceinline__ int64_t nr_sv_hdir(int64_t nb) { return nr_sv_h(8, nb); }
 __host__ __device__ __forceinline__ int64_t nr_sv_dirpe(int64_t nb) {
     return nr_sv_hdir(nb) + NR_NATIVE(128) * nb;
 }

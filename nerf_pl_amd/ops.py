@@ -35,12 +35,28 @@ if MATH not in MATHS:
 # csrc/layout.h NR_SAVE_PER_BLOCK / NR_GRAD_PER_BLOCK (block-native layout);
 # a save buffer ends with the f16x3 gradient statistics (nr_stats_floats:
 # NR_STATS reduced maxima, then NR_STAT_SEGS per-wave maxima per block)
-SAVE_PER_BLOCK = BLK * (64 + 8 * 256 + 256 + 128 + 32) + 9 * 256
+SAVE_PER_BLOCK = BLK * (64 + 8 * 256 + 128 + 32) + 9 * 256     # no feat segment (wgrad.hip task 10)
 SAVE_STATS, STAT_SEGS = 16, 11
+
+
+_LAYOUT_OK = False
+
+
+def _check_layout():
+    """The library's save / gradient block sizes must be this module's: a
+    library built from other sources would write past buffers sized here"""
+    global _LAYOUT_OK
+    if not _LAYOUT_OK:
+        got = (int(lib().nr_layout_query(3)), int(lib().nr_layout_query(4)))
+        if got != (SAVE_PER_BLOCK, GRAD_PER_BLOCK):
+            raise RuntimeError(f"nerf_pl_amd: libnerf_pl_amd.so has save/grad blocks {got}, the package "
+                               f"{(SAVE_PER_BLOCK, GRAD_PER_BLOCK)}: rebuild the library (make)")
+        _LAYOUT_OK = True
 
 
 def save_floats(n: int) -> int:
     """Floats of a training save buffer for n samples."""
+    _check_layout()
     nb = n_blocks(n)
     return nb * SAVE_PER_BLOCK + SAVE_STATS + STAT_SEGS * nb
 GRAD_PER_BLOCK = BLK * (9 * 256 + 128 + 4)
@@ -327,7 +343,7 @@ def save_segments(sv: torch.Tensor, n: int) -> dict:
     nb = n_blocks(n)
     o, out = 0, {}
     for name, w in [("pe", 64)] + [(f"h{i}", 256) for i in range(1, 9)] + \
-                   [("feat", 256), ("hdir", 128), ("dirpe", 32)]:
+                   [("hdir", 128), ("dirpe", 32)]:
         out[name] = sv[o:o + nb * BLK * w]
         o += nb * BLK * w
     out["mask"] = sv[o:o + nb * 9 * 256]
