@@ -74,13 +74,15 @@ FLOP_TRAIN_SIGMA = 2 * FLOP_FWD_SIGMA + 2 * (FLOP_FWD_SIGMA // 2 - 2 * 63 * 256)
 # weight gradient: algorithmic HBM bytes per sample (every saved segment read
 # once).  The forward saves 2272 activation values per sample (PE 64, h1..h8,
 # hdir 128, dir PE 32: xyz_encoding_final's output is not saved, the dir
-# layer's feat columns come from h8), the backward 2436 gradient values; the
-# kernels read h8 a second time for the dir layer's task (not counted here)
+# layer's feat columns come from h8), the backward 2180 gradient values
+# (dz1..dz8, dz_dir, head 4: d feat is not saved either -- xyz_encoding_final's
+# weight gradient is W_dir[:, :256]^T G with G = dz_dir^T h8, wgrad.hip task 10)
 SAVED_VALUES = 2272
-BYTES_WGRAD = 4 * (SAVED_VALUES + 2436)                     # 18,832
+GRAD_VALUES = 2180
+BYTES_WGRAD = 4 * (SAVED_VALUES + GRAD_VALUES)              # 17,808
 # bf16 variant: every segment stored in bf16 except the 4-float head gradient
-# (itself bf16 too: 8 B/sample) -> 2 * (2272 + 2436) = 9,416
-BYTES_WGRAD_BF16 = 2 * (SAVED_VALUES + 2436)
+# (itself bf16 too: 8 B/sample) -> 2 * (2272 + 2180) = 8,904
+BYTES_WGRAD_BF16 = 2 * (SAVED_VALUES + GRAD_VALUES)
 # the sigma-only graph trained on its own kernels (rendering_shadows.py:167):
 # data gradient without layer 1 and layer 5's PE columns; weight gradient of
 # xyz_encoding_1..8 + sigma, reading PE, h1..h8, dz1..dz8 and the head once
@@ -134,7 +136,7 @@ def kernel_roofline(k, events, math_, traffic_json):
         return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / HBM_PEAK_GBS, 4), bytes_per_sample=bps,
                     bytes_basis=(f"every saved activation ({SAVED_VALUES} values/sample) and gradient "
-                                 "(2436 values/sample) segment read once, " if k == "mlp_wgrad"
+                                 f"({GRAD_VALUES} values/sample) segment read once, " if k == "mlp_wgrad"
                                  else "the sigma-only graph's saved PE, h1..h8, dz1..dz8 and "
                                       "head (4164 values/sample) read once, ")
                                 + ("bf16" if math_ == "bf16" else "fp32"),

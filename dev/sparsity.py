@@ -113,12 +113,10 @@ def main():
         r["hdir"] = seg_zero(save, (64 + 8 * 256) * W32 * nb, 128, nb)   # no feat segment (round 5)
         for l in range(8):
             r[f"dz{l + 1}"] = seg_zero(gws, l * 256 * W32 * nb, 256, nb)
-        r["dfeat"] = seg_zero(gws, 8 * 256 * W32 * nb, 256, nb)
-        r["dzdir"] = seg_zero(gws, 9 * 256 * W32 * nb, 128, nb)
-        # the wgrad operand bytes (19,856 B/sample): values that are zero
-        widths = {"pe": 64, "hdir": 128, "dfeat": 256, "dzdir": 128}
+        r["dzdir"] = seg_zero(gws, 8 * 256 * W32 * nb, 128, nb)   # no dfeat segment (round 5)
+        # the wgrad operand bytes (17,808 B/sample): values that are zero
+        widths = {"pe": 64, "hdir": 128, "dzdir": 128}
         widths.update({f"h{l + 1}": 256 for l in range(8)})
-        widths["h8"] += 256     # read twice: tasks 9 and 10 (the dir layer's feat columns, round 5)
         widths.update({f"dz{l + 1}": 256 for l in range(8)})
         tot = sum(widths.values()) + 32 + 4 + 0   # + dir PE (32) + head (4): never zero
         r["zero_fraction_of_wgrad_values"] = round(

@@ -62,17 +62,10 @@ __host__ __device__ __forceinline__ int64_t nr_blocks_pad(int64_t n) { return ((
 #define NR_SAVE_PER_BLOCK (NR_NATIVE(64) + 8 * NR_NATIVE(256) + NR_NATIVE(128) + NR_NATIVE(32) + \
                            NR_MASK_LAYERS * 256)
 
-//   dz1..dz8, dfeat (256 wide), dzdir (128), dhead [block][j][4] = (dz_rgb, dsigma)
-#define NR_GRAD_PER_BLOCK (9 * NR_NATIVE(256) + NR_NATIVE(128) + NR_BLK * 4)
-struct NrGrad {
-    float* dz[8]; float* dfeat; float* dzdir; float* dhead;
-    __host__ __device__ NrGrad(float* base, int64_t nb) {
-        for (int l = 0; l < 8; ++l) dz[l] = base + (int64_t)l * NR_NATIVE(256) * nb;
-        dfeat = base + 8 * NR_NATIVE(256) * nb;
-        dzdir = dfeat + NR_NATIVE(256) * nb;
-        dhead = dzdir + NR_NATIVE(128) * nb;
-    }
-};
+//   dz1..dz8, dzdir (128), dhead [block][j][4] = (dz_rgb, dsigma).  dfeat (the
+//   gradient of xyz_encoding_final's output) is not stored: that layer's weight
+//   gradient is W_dir[:, :256]^T G, G = sum dz_dir h8^T (wgrad.hip task 10)
+#define NR_GRAD_PER_BLOCK (8 * NR_NATIVE(256) + NR_NATIVE(128) + NR_BLK * 4)
 
 // keep x where mask bit b of word w is set, else +0 (ReLU backward)
 __device__ __forceinline__ float nr_mask_bit(float x, uint32_t w, int b) {
@@ -105,10 +98,10 @@ __host__ __device__ __forceinline__ int64_t nr_sv_stats(int64_t nb) { return NR_
 __host__ __device__ __forceinline__ int64_t nr_stats_floats(int64_t nb) {
     return NR_STATS + NR_STAT_SEGS * nb;
 }
-__host__ __device__ __forceinline__ int64_t nr_gd_dz(int l, int64_t nb) {   // l = 0..8 (8 = dfeat)
+__host__ __device__ __forceinline__ int64_t nr_gd_dz(int l, int64_t nb) {   // l = 0..7
     return (int64_t)l * NR_NATIVE(256) * nb;
 }
-__host__ __device__ __forceinline__ int64_t nr_gd_dzdir(int64_t nb) { return nr_gd_dz(9, nb); }
+__host__ __device__ __forceinline__ int64_t nr_gd_dzdir(int64_t nb) { return nr_gd_dz(8, nb); }
 __host__ __device__ __forceinline__ int64_t nr_gd_dhead(int64_t nb) {
     return nr_gd_dzdir(nb) + NR_NATIVE(128) * nb;
 }

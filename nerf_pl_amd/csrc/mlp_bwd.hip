@@ -149,7 +149,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
                               [&](int grp) { store_native_piece<4>(C, grp, cdst, lane); });
     }
 
-    // d h8 = W_final^T dfeat + W_sigma^T dsigma, masked by h8; stores dfeat
+    // d h8 = W_final^T dfeat + W_sigma^T dsigma, masked by h8.  dfeat is not
+    // stored: xyz_encoding_final's weight gradient is W_dir[:, :256]^T G with
+    // G = sum dz_dir h8^T (wgrad.hip task 10, nr_wgrad_dir_feat)
 #pragma unroll
     for (int t = 0; t < 8; ++t)
 #pragma unroll
@@ -161,7 +163,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd_kernel(BwdArgs a) {
     {
         const uint4 mk = mask[7 * 64];
         nr_mm_chain<128, 8, 8>(PB + NR_B_FINALT, PB + NR_B_L8T, lane, B, wq,
-                               [&](int g) { return A[g >> 4][g & 15]; }, side8(A, dzseg(8)));
+                               [&](int g) { return A[g >> 4][g & 15]; });
         relu_mask<8>(B, mk);
     }
     }   // !SO

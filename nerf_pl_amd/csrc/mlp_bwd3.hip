@@ -88,9 +88,9 @@ __device__ __forceinline__ void report_max(float m, float* slot, int lane) {
 // 2s, p = 2, 3 tile 2s+1) for the weight-gradient GEMMs
 // f16x3: B values and stored values are scaled per sample (GScale); begin()
 // renormalises from the getter whose B values produced X
-template <int NF, bool MASK>
+template <int NF, bool MASK, bool STORE = true>
 struct GradU {
-    static constexpr bool kStores = true;
+    static constexpr bool kStores = STORE;
     static constexpr bool kPaired = false;
     const f32x4 (&X)[NF][2];
     float* dst;
@@ -121,11 +121,13 @@ struct GradU {
             x1 *= sc.ks[sb];
             sc.mx[sb] = fmaxf(sc.mx[sb], fmaxf(fabsf(x0), fabsf(x1)));
         }
-        if ((p & 1) == 0) {
-            pend[0] = t0;
-            pend[1] = t1;
-        } else {
-            store_n16(f32x4{pend[0], pend[1], t0, t1}, F, sb, dst, lane);
+        if constexpr (STORE) {
+            if ((p & 1) == 0) {
+                pend[0] = t0;
+                pend[1] = t1;
+            } else {
+                store_n16(f32x4{pend[0], pend[1], t0, t1}, F, sb, dst, lane);
+            }
         }
     }
     // after the last split: the segment's max |true value| -> its stats slot
@@ -338,7 +340,9 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         // d feat = W_dir[:, :256]^T dz_dir (xyz_encoding_final has no activation); stores dz_dir
         GradU<8, false> uc{C, GD + nr_gd_dzdir(nb) + (size_t)blk * NR_SEGF(128), {0u, 0u, 0u, 0u},
                            lane};
-        GradU<16, false> ua{A, dzseg(8), {0u, 0u, 0u, 0u}, lane};     // dfeat
+        // dfeat, not stored: xyz_encoding_final's weight gradient is
+        // W_dir[:, :256]^T G with G = sum dz_dir h8^T (wgrad.hip task 10)
+        GradU<16, false, false> ua{A, nullptr, {0u, 0u, 0u, 0u}, lane};
         // f16x3: the sigma head injects w_sigma dsigma (|.| <= max|w_sigma| |dsigma|)
         // into d h8.  The scales of dz_dir's and dfeat's B values are bounded by it
         // too, so the d h8 accumulator (which inherits dfeat's scale) stays finite

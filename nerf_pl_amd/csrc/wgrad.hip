@@ -1167,10 +1167,8 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
             case 5:    // DZ(4) x [H(3) | PE]: xyz_encoding_5 (skip layer)
                 wgrad_b1_body<256, 256, 2, 4, false, 1, 64>(a, T, b0, b1, lds, slab, xslab); break;
 #endif
-            case 9:    // [DZ(8) | head] x H(7): xyz_encoding_final and sigma
-                wgrad_b1_body<256, 256, 2, 4, false, 2, 4>(a, T, b0, b1, lds, slab, xslab); break;
-            case 10:   // dz_dir x [feat | dir PE]: dir_encoding
-                wgrad_b1_body<128, 256, 2, 4, false, 1, 32>(a, T, b0, b1, lds, slab, xslab); break;
+            case 10:   // [dz_dir | head] x H(7): dir_encoding's feat columns (as G) and sigma
+                wgrad_b1_body<128, 256, 2, 4, false, 2, 4>(a, T, b0, b1, lds, slab, xslab); break;
         }
 #else
         switch (__builtin_amdgcn_readfirstlane(T.id)) {
@@ -1182,13 +1180,8 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
                 break;
 #endif
 #if NR_WGRAD_FUSE_MASK & 2
-            case 9:    // [DZ(8) | head] x H(7): xyz_encoding_final and sigma
-                wgrad3_body<GA, ROWS, SEG_ACC, 256, SEG_ACC, 256, 2, 4, SEG_HEAD, 4, 1, 1, 8>(
-                    a, T, b0, b1, lds, slab, xslab); break;
-#endif
-#if NR_WGRAD_FUSE_MASK & 4
-            case 10:   // dz_dir x [feat | dir PE]: dir_encoding
-                wgrad3_body<GA, ROWS, SEG_ACC, 128, SEG_ACC, 256, 2, 4, SEG_DPE, 32, 0, 4, 1>(
+            case 10:   // [dz_dir | head] x H(7): dir_encoding's feat columns (as G) and sigma
+                wgrad3_body<GA, ROWS, SEG_ACC, 128, SEG_ACC, 256, 2, 4, SEG_HEAD, 4, 1, 1, 8>(
                     a, T, b0, b1, lds, slab, xslab); break;
 #endif
         }
@@ -1350,8 +1343,31 @@ __global__ void __launch_bounds__(256) dir_feat_kernel(const float* __restrict__
     row[c] = fmaf(grad[kP.b[9] + o], params[kP.b[8] + c], acc);
 }
 
+// xyz_encoding_final (nerf.py:116): dW = W_dir[:, :256]^T G, db = W_dir[:, :256]^T db_dir
+// (dfeat = W_dir[:, :256]^T dz_dir is not stored).  Runs before dir_feat_kernel
+// rewrites G.  Workgroup c = output row, thread k = column; fp32 fma chains over
+// the 128 dir outputs in order.
+__global__ void __launch_bounds__(256) final_from_g_kernel(const float* __restrict__ params,
+                                                          float* __restrict__ grad) {
+    const int c = blockIdx.x, k = threadIdx.x;
+    constexpr int kFan = 283;
+    const float* G = grad + kP.w[9];                 // G[o][k] at o * 283 + k
+    const float* W = params + kP.w[9];               // W_dir[o][c] at o * 283 + c
+    float acc = 0.f, b = 0.f;
+#pragma unroll 8
+    for (int o = 0; o < 128; ++o) {
+        const float w = W[o * kFan + c];
+        acc = fmaf(w, G[o * kFan + k], acc);
+        if (k == 0) b = fmaf(w, grad[kP.b[9] + o], b);
+    }
+    grad[kP.w[8] + c * 256 + k] = acc;
+    if (k == 0) grad[kP.b[8] + c] = b;
+}
+
 NR_API int nr_wgrad_dir_feat(const float* params, float* grad_flat, void* stream) {
     NR_REQUIRE(params && grad_flat, "nr_wgrad_dir_feat: null pointer");
+    final_from_g_kernel<<<256, 256, 0, (hipStream_t)stream>>>(params, grad_flat);
+    NR_LAUNCH_CHECK("nr_wgrad_dir_feat");
     dir_feat_kernel<<<128, 256, 0, (hipStream_t)stream>>>(params, grad_flat);
     NR_LAUNCH_CHECK("nr_wgrad_dir_feat");
     return 0;
@@ -1395,14 +1411,19 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     // task 10 (dir_encoding's feat columns) reads h8, not xyz_encoding_final's
     // output: dW = sum dz_dir feat^T = G W_final^T + db_dir b_final^T with
     // G = sum dz_dir h8^T (nerf.py:116, feat = W_final h8 + b_final), so the
-    // forward saves no feat; nr_wgrad_dir_feat finishes it
+    // forward saves no feat.  And task 9 (xyz_encoding_final) launches nothing:
+    // its dW = sum dfeat h8^T with dfeat = W_dir[:, :256]^T dz_dir is
+    // W_dir[:, :256]^T G (db = W_dir[:, :256]^T db_dir), so the data gradient
+    // stores no dfeat either.  nr_wgrad_dir_feat forms both from G
+    // (DESIGN.md 13); task 9's entry keeps the id order (its slot: a dummy)
     const WgSeg hdir = acc(SV + nr_sv_hdir(nbp), 128);
     const WgSeg dzdir = acc(GD + nr_gd_dzdir(nbp), 128);
     // (a, b, wm, wn); task order fixes wgrad_dest / wgrad_bias_dest
     const WgTask tasks[kTasks] = {
         {DZ(0), pe, 8, 1}, {DZ(1), H(0), 2, 4}, {DZ(2), H(1), 2, 4}, {DZ(3), H(2), 2, 4},
         {DZ(4), pe, 8, 1}, {DZ(4), H(3), 2, 4}, {DZ(5), H(4), 2, 4}, {DZ(6), H(5), 2, 4},
-        {DZ(7), H(6), 2, 4}, {DZ(8), H(7), 2, 4}, {dzdir, H(7), 2, 4}, {dzdir, dpe, 4, 1},
+        {DZ(7), H(6), 2, 4}, {DZ(0), H(7), 2, 4} /* 9: dummy, no workgroups */,
+        {dzdir, H(7), 2, 4}, {dzdir, dpe, 4, 1},
         {head, H(7), 1, 8}, {head, hdir, 1, 4},
     };
     WgArgs a{};
@@ -1453,7 +1474,7 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
         const int split = cost[t] >= heavy && tasks[t].a.kind != SEG_HEAD ? 1 : 3;
         int64_t g = split * ((target_wg * cost[t] + tot - 1) / tot);
         gt[t] = std::max<int64_t>(1, std::min<int64_t>(g, nb));
-        if (!((tmask >> t) & 1)) gt[t] = 0;
+        if (!((tmask >> t) & 1) || t == 9) gt[t] = 0;   // task 9: nr_wgrad_dir_feat
         pos[t] = k;
     }
     // f16x3: the tasks that read the same saved segment run fused (kFuse,
@@ -1461,7 +1482,10 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     // partner's output over the same block ranges into the partner's slabs, so
     // DZ(4), H(7) and dz_dir (2.5 KB/sample) are read once.  The partner keeps
     // its slabs and its reduction but launches no workgroups of its own.
-    static const int kFused[3][2] = {{5, 4}, {9, 12}, {10, 11}};   // {primary, partner}
+    // (round 5: task 9, xyz_encoding_final = DZ(8) x H(7), launches nothing --
+    // its gradient is W_dir[:, :256]^T G, nr_wgrad_dir_feat -- so the sigma
+    // head pairs with task 10, which reads H(7) too)
+    static const int kFused[2][2] = {{5, 4}, {10, 12}};   // {primary, partner}
     static const bool fuse_on = !getenv("NR_WGRAD_FUSE") || atoi(getenv("NR_WGRAD_FUSE")) != 0;
     int partner[kTasks];
     bool absorbed[kTasks];
@@ -1470,7 +1494,7 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
         // launches over a sample list have their own pair set (see target_wg)
         const int fmask = (slist && !NR_BF1) ? (NR_WGRAD_FUSE_MASK & NR_WGRAD_FUSE_MASK_GA)
                                              : NR_WGRAD_FUSE_MASK;
-        for (int i = 0; i < 3; ++i) {
+        for (int i = 0; i < 2; ++i) {
             if (!((fmask >> i) & 1)) continue;
             const auto& pr = kFused[i];
             if (!((tmask >> pr[0]) & 1) || !((tmask >> pr[1]) & 1)) continue;   // both must run

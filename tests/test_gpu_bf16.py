@@ -142,27 +142,34 @@ class _LinBF16(torch.autograd.Function):
         return dx, rb(dy).T @ rb(x), db, None, None
 
 
-class _DirBF16(torch.autograd.Function):
-    """dir_encoding (nerf.py:118-119) as the kernels form its gradient: forward
-    and data gradient as _LinBF16 on cat[feat, dir PE]; the weight gradient of
-    the feat columns from h8 -- (rb(dy)^T rb(h8)) W_final^T + db b_final^T
-    (feat = W_final h8 + b_final is not saved, wgrad.hip task 10 +
-    nr_wgrad_dir_feat) -- and of the dir PE columns rb(dy)^T rb(x)."""
+class _FinalDirBF16(torch.autograd.Function):
+    """xyz_encoding_final + dir_encoding (nerf.py:116-119) as the kernels form
+    their gradients: forward and data gradient as _LinBF16 (feat = rb(h8)
+    rb(W_final)^T + b_final, then rb([feat, dir PE]) rb(W_dir)^T + b_dir; d h8 =
+    rb(d feat) rb(W_final)); neither feat nor d feat is saved, so both weight
+    gradients come from G = rb(dy)^T rb(h8) (wgrad.hip task 10,
+    nr_wgrad_dir_feat): dW_dir's feat columns G W_final^T + db_dir b_final^T,
+    dW_final W_dir[:, :256]^T G, db_final W_dir[:, :256]^T db_dir; the dir PE
+    columns rb(dy)^T rb(x) as before."""
 
     @staticmethod
-    def forward(ctx, feat, xd, h8, w, b, wf, bf):
+    def forward(ctx, h8, xd, wf, bf, w, b):
+        feat = rb(h8) @ rb(wf).T + bf
         x = torch.cat([feat, xd], -1)
-        ctx.save_for_backward(x, h8, w, wf, bf)
+        ctx.save_for_backward(x, h8, wf, bf, w)
         return rb(x) @ rb(w).T + b
 
     @staticmethod
     def backward(ctx, dy):
-        x, h8, w, wf, bf = ctx.saved_tensors
-        dx = rb(dy) @ rb(w)
+        x, h8, wf, bf, w = ctx.saved_tensors
+        dfeat = (rb(dy) @ rb(w))[:, :256]
+        dh8 = rb(dfeat) @ rb(wf)
         db = rb(dy).sum(0)
+        G = rb(dy).T @ rb(h8)
         dw = rb(dy).T @ rb(x)
-        dw[:, :256] = (rb(dy).T @ rb(h8)) @ wf.T + db[:, None] * bf[None, :]
-        return dx[:, :256], None, None, dw, db, None, None
+        dw[:, :256] = G @ wf.T + db[:, None] * bf[None, :]
+        wdf = w[:, :256]
+        return dh8, None, wdf.T @ G, wdf.T @ db, dw, db
 
 
 def nerf_bf16_autograd(P, x):
@@ -177,10 +184,8 @@ def nerf_bf16_autograd(P, x):
             h = torch.cat([xe, h], -1)
         h = torch.relu(L(h, f"xyz_encoding_{i + 1}.0"))
     sigma = L(h, "sigma", False, False)
-    feat = L(h, "xyz_encoding_final")
-    hd = torch.relu(_DirBF16.apply(feat, xd, h, P["dir_encoding.0.weight"], P["dir_encoding.0.bias"],
-                                   P["xyz_encoding_final.weight"].detach(),
-                                   P["xyz_encoding_final.bias"].detach()))
+    hd = torch.relu(_FinalDirBF16.apply(h, xd, P["xyz_encoding_final.weight"], P["xyz_encoding_final.bias"],
+                                        P["dir_encoding.0.weight"], P["dir_encoding.0.bias"]))
     rgb = torch.sigmoid(L(hd, "rgb.0", False, False))
     return torch.cat([rgb, sigma], -1)
 
