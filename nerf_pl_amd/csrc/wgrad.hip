@@ -104,6 +104,9 @@ struct WgTask {
     int stat;            // f16x3: stats slot of the gradient operand (layout.h NR_STATS)
     int fuse;            // f16x3: index (in WgArgs::task) of the task whose output this task's
                          // workgroups also compute (same block ranges, its own slab), or -1
+    int pa, pb;          // slab row / column order (wgrad4_kernel): 1 natural; V: each
+                         // 32V-wide chunk holds its V interleaved MFMA tiles one after
+                         // another (w4_unperm)
 };
 
 struct WgArgs {
@@ -1220,6 +1223,465 @@ __global__ void __launch_bounds__(kThreads, 1) wgrad3_kernel(WgArgs a) {
     }
 }
 
+#ifndef NR_W4
+#define NR_W4 1
+#endif
+// slab index p (row or column) of a WgTask::pa / pb order -> the natural index
+__device__ __forceinline__ int w4_unperm(int p, int v) {
+    if (v <= 1) return p;
+    const int w = 32 * v, r = p % w;
+    return p - r + v * (r & 31) + (r >> 5);
+}
+#ifndef NR_W4_SGB
+#define NR_W4_SGB 0      // (unused)
+#endif
+// NR_W4_DBG (timing experiments only): 1 = no MFMAs (pieces kept alive),
+// 2 = no DMA after the prologue, 3 = no LDS reads / splits after the prologue
+#ifndef NR_W4_DBG
+#define NR_W4_DBG 0
+#endif
+
+#if NR_F16
+// ---------------------------------------------------------------------------
+// f16x3 weight gradient of the full graph, LDS-DMA form (round 5).  The
+// register-staged wgrad3_body holds two stages of both operands in VGPRs
+// next to its accumulators (two waves per SIMD: 8 spilled VGPRs), which caps
+// the bytes in flight per CU; its gathered rows waited ~half of the wave
+// cycles.  Here nothing is staged through registers: a workgroup of 4 waves
+// (one per SIMD, 512 VGPRs each) copies every 16-sample stage of both operands
+// into an LDS ring of kD stages with global_load_lds (3 stages = ~100 KiB in
+// flight per CU), and each wave reads its MFMA fragments from LDS as fp32 and
+// splits them into the f16 pieces itself, between the MFMAs of the previous
+// stage.  One wave's float4 read feeds four 32x32x16 tiles at once: lane c of a
+// 128-row chunk holds rows 4c .. 4c + 3, i.e. tile i of the chunk holds rows
+// 4 rho + i (the slab stores tiles in that order, the reduction undoes it,
+// WgTask::pa / pb).
+//   gradient operand (N16 slots by position): one 1-KiB instruction per
+//     16-feature piece, its lanes permuted so that the LDS piece is sample-major
+//     [sample 16][4 features x 4]; pieces 1088 B apart, so the float4 reads of
+//     one instruction's lane groups (x3.h / MICROARCH.md ds_read_b128 groups)
+//     fall in distinct banks;
+//   input operand (sample-major rows, gathered): one instruction per 1 KiB of
+//     rows (1 row of h, 4 PE rows, 8 dir-PE rows), LDS image [sample][W];
+//   sample list (GA): each wave DMAs the 16 list entries of stage t + 2kD - 1
+//     into its own slot of an index ring, so the row addresses of a stage come
+//     from LDS (ordinary loads would make the compiler drain vmcnt, and
+//     scalar loads would hold every LDS wait behind their latency).
+// A barrier per stage hands it over; positions >= m of the last stage are
+// zeroed in LDS.
+// ---------------------------------------------------------------------------
+namespace w4 {
+constexpr int kWaves = 4, kT = 256;
+constexpr int kD = 4;                          // ring stages of 16 samples
+constexpr int kPS = 1088;                      // LDS stride of a gradient piece (1 KiB + 64 B)
+constexpr int kAImg = 16 * kPS;                // gradient image (<= 16 pieces)
+constexpr int kBImg = 16 * 1024;               // input image (16 rows x <= 256 floats)
+constexpr int kHImg = 256;                     // head gradient [16][4]
+constexpr int kSlot = kAImg + kBImg + kHImg;   // 34,048 B
+constexpr int kIdxStages = 2 * kD;             // index ring
+constexpr int kIdxWave = 256;                  // one wave's copy of a stage's list entries (64 x 4 B)
+constexpr int kIdxOff = kD * kSlot;
+constexpr int kDummyOff = kIdxOff + kIdxStages * kWaves * kIdxWave;
+constexpr int kLds = kDummyOff + 256;          // 144,640 B
+typedef __attribute__((address_space(3))) void* lds_ptr;
+// buffer_load ... lds (the global_load_lds form makes the compiler wait
+// vmcnt(0) before every later DMA and LDS read: it cannot tell the ring slots
+// apart); voffset per lane, soffset uniform, byte offsets within the resource
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* l) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr)l, 16, voff, soff, 0, 0);
+}
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* l) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr)l, 4, voff, soff, 0, 0);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+template <int V> struct Vec { typedef float T __attribute__((ext_vector_type(V))); };
+template <> struct Vec<1> { typedef float T; };
+template <int V>
+__device__ __forceinline__ float vget(const typename Vec<V>::T& v, int j) {
+    if constexpr (V == 1) return v;
+    else return v[j];
+}
+// the pieces of 8 values as two fragments (x0..x7 times sc): built from packed
+// pairs, so each fragment stays 4 VGPRs (element-wise inserts into an f16x8
+// keep one half per register)
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split8(const float (&x)[8], float sc, x3::Pieces& f) {
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        x3::p2 q[x3::kNP];
+        x3::split_p2(x[2 * p] * sc, x[2 * p + 1] * sc, q);
+        hi[p] = __builtin_bit_cast(uint32_t, q[0]);
+        lo[p] = __builtin_bit_cast(uint32_t, q[1]);
+    }
+    f.hi = __builtin_bit_cast(x3::p8, (u32x4_t){hi[0], hi[1], hi[2], hi[3]});
+    f.lo = __builtin_bit_cast(x3::p8, (u32x4_t){lo[0], lo[1], lo[2], lo[3]});
+}
+// A x B over one 32x32x16 tile, f16x3 (small products first, as x3::mfma_xp)
+__device__ __forceinline__ f32x16 mfma3(const x3::Pieces& a, const x3::Pieces& b, f32x16 acc) {
+    acc = x3::mfma32(a.lo, b.hi, acc);
+    acc = x3::mfma32(a.hi, b.lo, acc);
+    return x3::mfma32(a.hi, b.hi, acc);
+}
+}  // namespace w4
+
+// One task's workgroup.  MA: rows of the gradient segment (256, 128; 0: the
+// task's gradient is the 4-row head); HD: the head gradient rides along as one
+// more row tile (MA > 0: the fused partner's, written to xslab); WB: columns
+// of the input segment, VB: columns per lane (float, float2, float4 reads);
+// NWA x NWB: the wave grid (128-row chunks x 32 VB-column chunks).
+template <bool GA, int MA, bool HD, int WB, int VB, int NWA, int NWB>
+__device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, int b0, int b1, char* lds,
+                                            float* __restrict__ slab, float* __restrict__ xslab) {
+    using namespace w4;
+    constexpr int NA = MA / 16;                   // gradient pieces per stage
+    constexpr int RPI = 256 / WB;                 // input rows per DMA instruction
+    constexpr int NBI = 16 / RPI;                 // input instructions per stage
+    constexpr int KA = NA / 4, KB = NBI / 4;      // per wave: gradient pieces, full input rounds
+    constexpr int RB = NBI % 4;                   // input instructions left over
+    constexpr int NX = (HD ? 1 : 0) + RB;         // leftover instructions (one slot per wave)
+    constexpr int K = KA + KB + (NX > 0 ? 1 : 0); // DMA instructions per wave and stage
+    constexpr int KV = K + (GA ? 1 : 0);          // vm instructions per wave and issue step
+    static_assert(NA % 4 == 0 && NX <= kWaves, "DMA assignment");
+    constexpr int TA = (MA ? 4 : 0) + (HD ? 1 : 0);
+    constexpr int HT = MA ? 4 : 0;                // the head's tile index
+    constexpr int RSB = WB * 4;                   // input row stride in LDS (bytes)
+    static_assert(NWA * NWB <= kWaves && NWB * 32 * VB == WB && (MA == 0 ? NWA == 1 : NWA * 128 == MA),
+                  "wave grid");
+    static_assert(RPI * NBI == 16 && WB * 4 * 16 <= kBImg && MA <= 256, "stage geometry");
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c = lane & 31, h = lane >> 5;
+    const int wa = wave / NWB, wb = wave % NWB;
+    const bool active = wave < NWA * NWB;
+    const int m = wg_m(a);
+    const int nst = 2 * (b1 - b0);
+    const int blast = b1 > b0 ? b1 - 1 : b0;
+    const int mlast = max(m - 1, 0);
+    const float* Abase = T.a.base;
+    const float* Hbase = MA ? (HD ? a.task[T.fuse].a.base : T.a.base) : T.a.base;
+    const float* Bbase = T.b.base;
+    const float sca = task_scale(a, T);
+    const float sch = HD && MA ? task_scale(a, a.task[T.fuse]) : sca;
+    float* hslab = MA ? xslab : slab;             // the head tile's output
+
+    auto q0_of = [&](int t) { return min(b0 + (t >> 1), blast) * 32 + 16 * (t & 1); };
+    auto idx_slot = [&](int u) {
+        return lds + kIdxOff + (u % kIdxStages) * (kWaves * kIdxWave) + wave * kIdxWave;
+    };
+    // buffer resources (the host keeps every segment under 2 GiB: wgrad_launch)
+    const __amdgpu_buffer_rsrc_t ra = rsrc(Abase, (int64_t)a.nb * (MA ? MA : 4) * 128);
+    const __amdgpu_buffer_rsrc_t rh = rsrc(Hbase, (int64_t)a.nb * 512);
+    const __amdgpu_buffer_rsrc_t rb = rsrc(Bbase, (int64_t)a.n * WB * 4);
+    const __amdgpu_buffer_rsrc_t rl = rsrc(a.slist, GA ? (int64_t)a.n * 4 : 0);
+    auto idx_dma = [&](int u) {     // list entries q0(u) .. +63 (clamped) -> this wave's index slot
+        dma4(rl, 4 * min(q0_of(u) + lane, mlast), 0, idx_slot(u));
+    };
+    // one issue step: stage t's DMA into ring slot t % kD (+ the list entries of
+    // stage t + 2kD - 1).  Wave w issues gradient pieces w + 4k and input
+    // instructions w + 4k (types fixed per k), then one leftover slot: the head,
+    // the input instructions past a multiple of 4, or a dummy
+    const int voff_a = 16 * (16 * (lane & 3) + (lane >> 2));
+    auto b_dma = [&](char* slot, const int* idx, int q0, int r, int s1) {
+        if constexpr (RPI == 1) {           // one row per instruction: uniform sample s1
+            dma16(rb, 16 * lane, s1 * (WB * 4), slot + kAImg + r * 1024);
+        } else {
+            const int row = r * RPI + lane / (WB / 4);
+            const int s = GA ? idx[row] : min(q0 + row, mlast);
+            dma16(rb, s * (WB * 4) + 16 * (lane % (WB / 4)), 0, slot + kAImg + r * 1024);
+        }
+    };
+    // the uniform samples of this wave's one-row instructions of stage t (rows
+    // wave * KB + k), from the index ring (one LDS read) or by position
+    struct Rows { int s[KB > 0 ? KB : 1]; };
+    auto rows_of = [&](int t) {
+        Rows r{};
+        if constexpr (RPI == 1) {
+            if constexpr (GA) {
+                static_assert(KB == 4, "one float4 of list entries per wave");
+                const int4 v = *reinterpret_cast<const int4*>(idx_slot(t) + 16 * wave);
+                r.s[0] = __builtin_amdgcn_readfirstlane(v.x);
+                r.s[1] = __builtin_amdgcn_readfirstlane(v.y);
+                r.s[2] = __builtin_amdgcn_readfirstlane(v.z);
+                r.s[3] = __builtin_amdgcn_readfirstlane(v.w);
+            } else {
+#pragma unroll
+                for (int k = 0; k < KB; ++k) r.s[k] = min(q0_of(t) + wave * KB + k, mlast);
+            }
+        }
+        return r;
+    };
+    // instruction k (< KV) of this wave's issue step for stage t
+    auto issue_k = [&](int t, int k, const Rows& rw) {
+        char* slot = lds + (t % kD) * kSlot;
+        const int q0 = q0_of(t);
+        const int blk = q0 >> 5, hb = (q0 >> 4) & 1;
+        const int* idx = reinterpret_cast<const int*>(idx_slot(t));
+        if (k < KA) {
+            const int i = wave + 4 * k;     // piece i: lane 4j + g <- float4 (g, sample j)
+            dma16(ra, voff_a, blk * (MA * 128) + (i * 2 + hb) * 1024, slot + i * kPS);
+        } else if (k < KA + KB) {
+            const int r = wave * KB + k - KA;
+            b_dma(slot, idx, q0, r, rw.s[(k - KA) % (KB > 0 ? KB : 1)]);
+        } else if (NX > 0 && k == KA + KB) {
+            const int r = 4 * KB + wave - (HD ? 1 : 0);   // an input instruction left over
+            if (HD && wave == 0) dma4(rh, 4 * lane, (blk * 32 + 16 * hb) * 16, slot + kAImg + kBImg);
+            else if (wave - (HD ? 1 : 0) < RB)
+                b_dma(slot, idx, q0, r, RPI == 1 ? (GA ? idx[r] : min(q0 + r, mlast)) : 0);
+            else dma4(ra, 4 * lane, 0, lds + kDummyOff);   // keeps every wave's vm count per step equal
+        } else if (GA) {
+            idx_dma(t + 2 * kD - 1);
+        }
+    };
+    auto issue = [&](int t) {
+        const Rows rw = rows_of(t);
+#pragma unroll
+        for (int k = 0; k < KV; ++k) issue_k(t, k, rw);
+    };
+    // positions >= m of stage t (the launch's last block): zero both operands in LDS
+    auto mask_tail = [&](int t) {
+        const int nval = m - q0_of(t);
+        if (t >= nst || nval >= 16) return;
+        char* slot = lds + (t % kD) * kSlot;
+        const int j0 = max(nval, 0);
+        if constexpr (NA > 0)
+            for (int e = tid; e < (16 - j0) * 16 * NA; e += kT) {   // 16 dwords per piece and sample
+                const int j = j0 + e / (16 * NA), r = e % (16 * NA);
+                reinterpret_cast<float*>(slot + (r >> 4) * kPS + 64 * j)[r & 15] = 0.f;
+            }
+        for (int e = tid; e < (16 - j0) * WB; e += kT)
+            reinterpret_cast<float*>(slot + kAImg + j0 * RSB)[e] = 0.f;
+        if (HD)
+            for (int e = tid; e < (16 - j0) * 4; e += kT)
+                reinterpret_cast<float*>(slot + kAImg + kBImg + j0 * 16)[e] = 0.f;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    f32x16 acc[TA][VB];
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+        for (int j = 0; j < VB; ++j) acc[i][j] = f32x16{};
+    float bs[4] = {0.f, 0.f, 0.f, 0.f}, hs = 0.f;
+
+    // fragments of stage t: ds_read_b32 of one row / column and 8 samples per
+    // lane (lanes c of a 32-lane half: 32 consecutive features, conflict-free
+    // in both images), split into the f16 pieces right away
+    auto split_a = [&](int t, int i, x3::Pieces& f) {
+        const char* slot = lds + (t % kD) * kSlot;
+        float x[8];
+        if (HD && i == HT) {
+            const float* ph = reinterpret_cast<const float*>(slot + kAImg + kBImg + 128 * h) + (c & 3);
+            float sum = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { x[k] = c < 4 ? ph[4 * k] : 0.f; sum += x[k]; }
+            hs += t < nst ? sum : 0.f;      // (stage nst: the clamped read past the end)
+            split8(x, sch, f);
+        } else if constexpr (MA > 0) {
+            const int fe = 128 * wa + 32 * i + c;
+            const float* pa = reinterpret_cast<const float*>(slot + (fe >> 4) * kPS + 512 * h) + (fe & 15);
+            float sum = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { x[k] = pa[16 * k]; sum += x[k]; }
+            bs[i & 3] += t < nst ? sum : 0.f;
+            split8(x, sca, f);
+        }
+    };
+    auto split_b = [&](int t, int j, x3::Pieces& f) {
+        const float* pb = reinterpret_cast<const float*>(lds + (t % kD) * kSlot + kAImg + 8 * h * RSB) +
+                          32 * VB * wb + 32 * j + c;
+        float x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = pb[k * WB];
+        split8(x, 1.f, f);
+    };
+    // wide form (VB > 1 / the gradient chunk): lane c holds rows 4c .. 4c + 3 of
+    // its 128-row chunk (columns VB c .. VB c + VB - 1 of its column chunk), so
+    // one ds_read_b128 (b64) per sample feeds 4 (VB) tiles: tile i holds rows
+    // 4 rho + i.  8 + 8 wide reads per stage instead of 32 + 32 ds_read_b32
+    // (one wave per SIMD issues those at a fraction of the LDS rate).  The
+    // slab is written in that order (WgTask::pa / pb, undone by the reduction).
+    using BV = typename Vec<VB>::T;
+    struct RawA { f32x4 v[MA > 0 ? 8 : 1]; };
+    struct RawB { BV v[8]; };
+    auto read_a = [&](int t, RawA& r) {
+        if constexpr (MA > 0) {
+            const char* pa = lds + (t % kD) * kSlot + (8 * wa + (c >> 2)) * kPS + 512 * h + 16 * (c & 3);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r.v[k] = *reinterpret_cast<const f32x4*>(pa + 64 * k);
+        }
+    };
+    auto read_b = [&](int t, RawB& r) {
+        const char* pb = lds + (t % kD) * kSlot + kAImg + 8 * h * RSB + (32 * VB * wb + VB * c) * 4;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r.v[k] = *reinterpret_cast<const BV*>(pb + k * RSB);
+    };
+    auto split_a_raw = [&](int t, const RawA& r, int i, x3::Pieces& f) {
+        if (HD && i == HT) { split_a(t, i, f); return; }
+        if constexpr (MA > 0) {
+            float x[8], sum = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { x[k] = r.v[k][i & 3]; sum += x[k]; }
+            if (wb == 0) bs[i & 3] += t < nst ? sum : 0.f;
+            split8(x, sca, f);
+        }
+    };
+    auto split_b_raw = [&](const RawB& r, int j, x3::Pieces& f) {
+        float x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = vget<VB>(r.v[k], j);
+        split8(x, 1.f, f);
+    };
+
+    // (nst == 0: the clamped, bounds-checked DMAs of block b0 run, nothing is
+    // multiplied and the slab is written as zeros)
+    {
+        if constexpr (GA) {
+#pragma unroll 1
+            for (int u = 0; u < 2 * kD - 1; ++u) idx_dma(u);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int t = 0; t < kD; ++t) issue(t);
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((kD - 1) * KV) : "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        mask_tail(0);
+        // pieces of the stage being multiplied: row tiles fa (each rewritten with
+        // the next stage's right after its MFMAs issued), column tiles fb (the
+        // next stage's go to fn first: every row tile still reads them)
+        // every wave multiplies (a wave outside the grid reads in-bounds LDS
+        // and writes nothing): no branch around the accumulators
+        x3::Pieces fa[TA], fb[VB];
+        {
+            RawA r0;
+            RawB q0;
+            read_a(0, r0);
+            read_b(0, q0);
+#pragma unroll
+            for (int i = 0; i < TA; ++i) split_a_raw(0, r0, i, fa[i]);
+#pragma unroll
+            for (int j = 0; j < VB; ++j) split_b_raw(q0, j, fb[j]);
+        }
+#pragma unroll 1
+        for (int s = 0; s < nst; ++s) {
+            // stage s + 1 landed (every wave's DMA) and stage s's slot is no longer read
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((kD - 2) * KV) : "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            mask_tail(s + 1);
+            // stage s + kD's DMA goes out between this stage's MFMAs (its list
+            // entries read first: one LDS read, used a row tile later)
+            const Rows rw = rows_of(s + kD);
+            x3::Pieces fn[VB];
+            RawA ra1;
+            RawB rb1;
+            if (NR_W4_DBG != 3) { read_a(s + 1, ra1); read_b(s + 1, rb1); }
+            // row tile i: its MFMAs (products outermost: VB independent
+            // accumulators between dependent ones), a share of the DMA, then
+            // the split of the next stage's column tiles (i = 0) or of row tile
+            // i - 1 (whose MFMAs have issued)
+#pragma unroll
+            for (int i = 0; i < TA; ++i) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+#pragma unroll
+                    for (int j = 0; j < VB; ++j) {
+                        if (NR_W4_DBG == 1) { asm volatile("" ::"v"(fa[i].lo), "v"(fa[i].hi), "v"(fb[j].lo), "v"(fb[j].hi)); continue; }
+                        acc[i][j] = p == 0 ? x3::mfma32(fa[i].lo, fb[j].hi, acc[i][j])
+                                  : p == 1 ? x3::mfma32(fa[i].hi, fb[j].lo, acc[i][j])
+                                           : x3::mfma32(fa[i].hi, fb[j].hi, acc[i][j]);
+                        asm volatile("" : "+a"(acc[i][j]));   // accumulators stay in AGPRs
+                    }
+#pragma unroll
+                for (int k = i * KV / TA; k < (i + 1) * KV / TA; ++k)
+                    if (NR_W4_DBG != 2) issue_k(s + kD, k, rw);
+                if (NR_W4_DBG == 3) continue;
+                if (i == 0) {
+#pragma unroll
+                    for (int j = 0; j < VB; ++j) split_b_raw(rb1, j, fn[j]);
+                } else {
+                    split_a_raw(s + 1, ra1, i - 1, fa[i - 1]);
+                }
+            }
+            if (NR_W4_DBG == 3) continue;
+            split_a_raw(s + 1, ra1, TA - 1, fa[TA - 1]);
+#pragma unroll
+            for (int j = 0; j < VB; ++j) fb[j] = fn[j];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped DMAs past the end
+    }
+    if (!active) return;
+    // bias sums: lanes c (h = 0, 1: samples 0..7, 8..15 of each stage)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bs[i] += __shfl_xor(bs[i], 32);
+    hs += __shfl_xor(hs, 32);
+    if (wb == 0 && h == 0) {
+        if constexpr (MA > 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) slab[MA * WB + 128 * wa + 4 * c + i] = bs[i];
+        }
+        if constexpr (HD) if (c < 4) hslab[4 * WB + c] = hs;
+    }
+    // tile (i, j) to slab rows 128 wa + 32 i + rho, columns 32 VB wb + 32 j + c
+    // (the natural row 128 wa + 4 rho + i, column 32 VB wb + VB c + j: w4_unperm)
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+        for (int j = 0; j < VB; ++j) {
+            const f32x16 v = acc[i][j];
+            const int cc = 32 * VB * wb + 32 * j + c;
+            float* dst = HD && i == HT ? hslab + cc : slab + (128 * wa + 32 * i) * WB + cc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rho = nr_acc_row(r, h);
+                if (!(HD && i == HT) || rho < 4) dst[rho * WB] = v[r];
+            }
+        }
+}
+
+// GA: gathered input rows (the *_active entry points), else by position
+template <bool GA>
+__global__ void __launch_bounds__(w4::kT, 1) wgrad4_kernel(WgArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[w4::kLds];
+    int t = 0;
+#pragma unroll 1
+    while (t + 1 < kTasks && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
+    const int c = blockIdx.x - a.wg_start[t];
+    const WgTask& T = a.task[t];
+    const int nact = wg_nact(a);
+    const int b0 = (int)((int64_t)c * nact / T.G);
+    const int b1 = (int)((int64_t)(c + 1) * nact / T.G);
+    float* slab = a.slab + T.slab + (int64_t)c * (T.a.width * T.b.width + T.a.width);
+    const int fu = __builtin_amdgcn_readfirstlane(T.fuse);
+    float* xslab = nullptr;
+    if (fu >= 0) {
+        const WgTask& P = a.task[fu];
+        xslab = a.slab + P.slab + (int64_t)c * (P.a.width * P.b.width + P.a.width);
+    }
+    switch (__builtin_amdgcn_readfirstlane(T.id)) {
+        case 0: case 4:     // DZ x PE
+            wgrad4_body<GA, 256, false, 64, 1, 2, 2>(a, T, b0, b1, lds, slab, xslab); break;
+        case 10:            // dz_dir x h8 (the dir layer's feat columns as G) [+ the sigma head, task 12]
+            if (fu >= 0) wgrad4_body<GA, 128, true, 256, 2, 1, 4>(a, T, b0, b1, lds, slab, xslab);
+            else wgrad4_body<GA, 128, false, 256, 2, 1, 4>(a, T, b0, b1, lds, slab, xslab);
+            break;
+        case 11:            // dz_dir x dir PE
+            wgrad4_body<GA, 128, false, 32, 1, 1, 1>(a, T, b0, b1, lds, slab, xslab); break;
+        case 12:            // head x h8
+            wgrad4_body<GA, 0, true, 256, 2, 1, 4>(a, T, b0, b1, lds, slab, xslab); break;
+        case 13:            // head x hdir
+            wgrad4_body<GA, 0, true, 128, 1, 1, 4>(a, T, b0, b1, lds, slab, xslab); break;
+        default:            // DZ x h
+            wgrad4_body<GA, 256, false, 256, 4, 2, 2>(a, T, b0, b1, lds, slab, xslab); break;
+    }
+}
+#endif  // NR_F16
+
 // Embedding channel of bf16x6 PE slot q (packing._pe16_channel / _dir16_channel)
 __device__ __forceinline__ int pe16_channel(int q) {
     if (q == 58 || q == 59) return q - 58;
@@ -1303,7 +1765,8 @@ __global__ void wgrad_reduce_kernel(WgArgs a, float* __restrict__ grad) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     const int nw = M * N, sz = nw + M;
     if (e >= sz) return;
-    const int dst = e < nw ? wgrad_dest(T.id, e / N, e % N, a.x3) : wgrad_bias_dest(T.id, e - nw);
+    const int dst = e < nw ? wgrad_dest(T.id, w4_unperm(e / N, T.pa), w4_unperm(e % N, T.pb), a.x3)
+                           : wgrad_bias_dest(T.id, e - nw);
     if (dst < 0) return;
     // 8 independent partial sums (fixed order: bitwise reproducible) keep 8
     // slab loads in flight per thread instead of one dependent chain
@@ -1486,13 +1949,23 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     // its gradient is W_dir[:, :256]^T G, nr_wgrad_dir_feat -- so the sigma
     // head pairs with task 10, which reads H(7) too)
     static const int kFused[2][2] = {{5, 4}, {10, 12}};   // {primary, partner}
+    // f16x3, full graph: the LDS-DMA weight gradient (wgrad4_kernel; NR_W4=0 at
+    // build time: the register-staged wgrad3_kernel)
+    // (32-bit buffer offsets: every segment it reads stays under 2 GiB below 2M samples)
+    // (NR_WGRAD_W4=0 in the environment: the register-staged kernel, for A/B
+    // runs and the cross-check test; read per launch)
+    const char* w4_env = getenv("NR_WGRAD_W4");
+    const bool use_w4 = NR_F16 && NR_W4 && !sigma_only && n < ((int64_t)1 << 21) &&
+                        !(w4_env && atoi(w4_env) == 0);
     static const bool fuse_on = !getenv("NR_WGRAD_FUSE") || atoi(getenv("NR_WGRAD_FUSE")) != 0;
     int partner[kTasks];
     bool absorbed[kTasks];
     for (int t = 0; t < kTasks; ++t) { partner[t] = -1; absorbed[t] = false; }
     if (kFuse && x3 && fuse_on && (tmask_env == -1)) {
         // launches over a sample list have their own pair set (see target_wg)
-        const int fmask = (slist && !NR_BF1) ? (NR_WGRAD_FUSE_MASK & NR_WGRAD_FUSE_MASK_GA)
+        // (wgrad4_kernel fuses the sigma head into task 10 only)
+        const int fmask = use_w4 ? 2
+                        : (slist && !NR_BF1) ? (NR_WGRAD_FUSE_MASK & NR_WGRAD_FUSE_MASK_GA)
                                              : NR_WGRAD_FUSE_MASK;
         for (int i = 0; i < 2; ++i) {
             if (!((fmask >> i) & 1)) continue;
@@ -1513,6 +1986,12 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
         a.task[k].G = (int)g;
         a.task[k].slab = slab;
         a.task[k].fuse = partner[t] >= 0 ? pos[partner[t]] : -1;
+        // wgrad4_kernel's slab orders: gradient rows 4-interleaved (not the head's), input
+        // columns VB-interleaved (its dispatch below)
+        static const int kW4Pa[kTasks] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 1, 1};
+        static const int kW4Pb[kTasks] = {1, 4, 4, 4, 1, 4, 4, 4, 4, 4, 2, 1, 2, 1};
+        a.task[k].pa = use_w4 ? kW4Pa[t] : 1;
+        a.task[k].pb = use_w4 ? kW4Pb[t] : 1;
         slab += g * (tasks[t].a.width * tasks[t].b.width + tasks[t].a.width);
         a.wg_start[k + 1] = a.wg_start[k] + (absorbed[t] ? 0 : (int)g);
     }
@@ -1526,7 +2005,9 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
 #if NR_F16
     stats_reduce_kernel<<<NR_STAT_SEGS, kStatT, 0, st>>>(SV + nr_sv_stats(nbp), (int)nbp);
     NR_LAUNCH_CHECK("nr_wgrad_stats");
-    if (slist && gather && !sigma_only) wgrad3_kernel<true, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
+    if (use_w4 && slist && gather) wgrad4_kernel<true><<<a.wg_start[kTasks], w4::kT, 0, st>>>(a);
+    else if (use_w4) wgrad4_kernel<false><<<a.wg_start[kTasks], w4::kT, 0, st>>>(a);
+    else if (slist && gather && !sigma_only) wgrad3_kernel<true, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else if (slist && gather) wgrad3_kernel<true, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else if (!sigma_only) wgrad3_kernel<false, true><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);
     else wgrad3_kernel<false, false><<<a.wg_start[kTasks], kThreads, 0, st>>>(a);

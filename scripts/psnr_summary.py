@@ -3,13 +3,13 @@ within 0.1 dB of the reference"; runs from scripts/psnr.sh).
 
 Groups of scripts/psnr_compare.py runs (2000 steps, PSNR at 500/1000/1500/2000,
 fine rgb on 2 held-out views; unperturbed runs only):
-  f16x3      this package, default arithmetic   profiles/r0[34]/psnr/f16x3_s*.json
-  fp32       this package, exact fp32 MFMA      profiles/r0[34]/psnr/fp32_s*.json
-  bf16       this package, the reduced-precision bf16 variant   profiles/r0[34]/psnr/bf16_s*.json
+  f16x3      this package, default arithmetic   profiles/r0[345]/psnr/f16x3_s*.json
+  fp32       this package, exact fp32 MFMA      profiles/r0[345]/psnr/fp32_s*.json
+  bf16       this package, the reduced-precision bf16 variant   profiles/r0[345]/psnr/bf16_s*.json
   ref_gpu    the reference's algorithm in PyTorch fp32 on the MI355X (the oracle,
-             pinned bit-exact to the reference; hipBLAS GEMMs)   profiles/r0[34]/psnr/oracle_s*.json
+             pinned bit-exact to the reference; hipBLAS GEMMs)   profiles/r0[345]/psnr/oracle_s*.json
   ref_cpu    the reference itself, CPU, here    profiles/r01/psnr_reference_s*.json,
-             profiles/r02/psnr/reference_s*.json, profiles/r0[34]/psnr/reference_s*.json
+             profiles/r02/psnr/reference_s*.json, profiles/r0[345]/psnr/reference_s*.json
 Per checkpoint: each group's n / mean / std, and for every pair the difference
 of the means, its standard error (Welch), the 95% interval and whether that
 interval lies inside +-0.1 dB.  Paired too ("paired"): runs of the same draw
@@ -17,8 +17,8 @@ seed start from the same parameters and see the same ray batches and the same
 render draws, so their PSNRs are correlated (r ~ 0.5-0.7) and the per-seed
 difference has a smaller spread than two independent samples; mean and
 Student-t interval of the per-seed differences over the seeds both groups ran.
-Writes profiles/r04/psnr/summary.json (round 3's runs under profiles/r03/psnr
-and round 4's under profiles/r04/psnr, one group per seed).
+Writes profiles/r05/psnr/summary.json (round 3's runs under profiles/r03/psnr,
+round 4's under profiles/r04/psnr and round 5's under profiles/r05/psnr, one group per seed).
 
     python scripts/psnr_summary.py
 """
@@ -64,12 +64,12 @@ def t975(df):
 
 def main():
     groups = {
-        "f16x3": load("profiles/r0[34]/psnr/f16x3_s*.json"),
-        "fp32": load("profiles/r0[34]/psnr/fp32_s*.json"),
-        "bf16": load("profiles/r0[34]/psnr/bf16_s*.json"),
-        "ref_gpu": load("profiles/r0[34]/psnr/oracle_s*.json"),
+        "f16x3": load("profiles/r0[345]/psnr/f16x3_s*.json"),
+        "fp32": load("profiles/r0[345]/psnr/fp32_s*.json"),
+        "bf16": load("profiles/r0[345]/psnr/bf16_s*.json"),
+        "ref_gpu": load("profiles/r0[345]/psnr/oracle_s*.json"),
         "ref_cpu": load("profiles/r01/psnr_reference_s*.json", "profiles/r02/psnr/reference_s*.json",
-                        "profiles/r0[34]/psnr/reference_s*.json"),
+                        "profiles/r0[345]/psnr/reference_s*.json"),
     }
     groups["ref_all"] = {("g", s): v for s, v in groups["ref_gpu"].items()}
     groups["ref_all"].update({("c", s): v for s, v in groups["ref_cpu"].items()})
@@ -120,7 +120,7 @@ def main():
                 "ci95_within_0.1dB": bool(abs(m) + half <= 0.1), "n": n, "corr": round(r, 2)}
         out["checkpoints"].append(row)
         print(json.dumps(row))
-    path = os.path.join(REPO, "profiles", "r04", "psnr", "summary.json")
+    path = os.path.join(REPO, "profiles", "r05", "psnr", "summary.json")
     os.makedirs(os.path.dirname(path), exist_ok=True)
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
