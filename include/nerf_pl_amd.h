@@ -294,7 +294,12 @@ int nr_mlp_bwd(const float* packed_bwd, const float* head, const float* out,
  * dir_encoding.0.weight's first 256 columns, and nr_wgrad_dir_feat, given the
  * flat fp32 parameters the forward ran with, turns them into the gradient
  * G W_final^T + d(bias_dir) b_final^T (feat = W_final h8 + b_final,
- * nerf.py:116-118; replaces autograd's sum dz_dir feat^T). */
+ * nerf.py:116-118; replaces autograd's sum dz_dir feat^T).  The data gradient
+ * does not save d feat either: the same call writes xyz_encoding_final's
+ * gradients W_dir[:, :256]^T G (weight) and W_dir[:, :256]^T d(bias_dir)
+ * (bias) -- autograd's sum d feat h8^T and sum d feat with
+ * d feat = W_dir[:, :256]^T dz_dir (nerf.py:116-119); the nr_wgrad* launch
+ * itself leaves that layer's slots zero. */
 int64_t nr_wgrad_workspace_bytes(int64_t n);
 int nr_wgrad(const float* save, const float* grad_ws, int64_t n, float* workspace,
              float* grad_flat, void* stream);

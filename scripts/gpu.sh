@@ -21,6 +21,7 @@
 #                   (dev/trained_step.py)
 #   defer_sweep     the deferral crossover on weights after 100 / 300 / 1000 / 2000 steps
 #   randperm        VERDICT r4 item 6: the pre-fix sampler's 64M device randperm, kernel trace
+#   emptylist       VERDICT r4 item 5: listed launches with 0 / 20% / all samples listed (dev/empty_list_probe.py)
 # Every profiling pass is its own rocprofv3 run with --kernel-trace only besides --pmc.
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -109,6 +110,11 @@ for step in "$@"; do
         --save-weights "$out/w_$st.safetensors" --out "$out/train_$st.json"
       run step_$st 200 python dev/trained_step.py "$out/w_$st.safetensors" --steps 40 --modes all,none,auto \
         --out "$out/step_$st.json"
+    done ;;
+  emptylist)
+    for f in 0 0.2 1; do
+      run empty_$f 200 rocprofv3 --kernel-trace --stats -d "$out/empty_$f" -o run --output-format csv -- \
+        python dev/empty_list_probe.py --frac $f
     done ;;
   randperm)
     run randperm 300 rocprofv3 --kernel-trace --stats -d "$out/randperm" -o probe --output-format csv -- \

@@ -27,7 +27,7 @@ import sys
 
 # (substring of the kernel name, tag); fp32 names are prefixes of none of the split ones
 KERNELS = [("mlp_fwd3_kernel", "mlp_fwd"), ("mlp_bwd3_kernel", "mlp_bwd_dgrad"),
-           ("wgrad3_kernel", "mlp_wgrad"), ("mlp_fwd_kernel", "fp32/mlp_fwd"),
+           ("wgrad3_kernel", "mlp_wgrad"), ("wgrad4_kernel", "mlp_wgrad"), ("mlp_fwd_kernel", "fp32/mlp_fwd"),
            ("mlp_bwd_kernel", "fp32/mlp_bwd_dgrad"), ("wgrad_kernel", "fp32/mlp_wgrad")]
 
 
