@@ -1236,6 +1236,7 @@ __device__ __forceinline__ int w4_unperm(int p, int v) {
 #define NR_W4_SGB 0      // (unused)
 #endif
 // NR_W4_DBG (timing experiments only): 1 = no MFMAs (pieces kept alive),
+// 4 = splits reduced to the hi conversion (no scale, no residual),
 // 2 = no DMA after the prologue, 3 = no LDS reads / splits after the prologue
 #ifndef NR_W4_DBG
 #define NR_W4_DBG 0
@@ -1311,6 +1312,11 @@ __device__ __forceinline__ void split8(const float (&x)[8], float sc, x3::Pieces
     uint32_t hi[4], lo[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
+#if NR_W4_DBG == 4      // timing experiment: hi pieces only, unscaled (wrong results)
+        (void)sc;
+        hi[p] = lo[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector((x3::f32x2){x[2 * p], x[2 * p + 1]}, x3::f16x2));
+        continue;
+#endif
         x3::p2 q[x3::kNP];
         x3::split_p2(x[2 * p] * sc, x[2 * p + 1] * sc, q);
         hi[p] = __builtin_bit_cast(uint32_t, q[0]);
@@ -1526,7 +1532,7 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
             float x[8], sum = 0.f;
 #pragma unroll
             for (int k = 0; k < 8; ++k) { x[k] = r.v[k][i & 3]; sum += x[k]; }
-            if (wb == 0) bs[i & 3] += t < nst ? sum : 0.f;
+            if (wb == 0 && NR_W4_DBG != 4) bs[i & 3] += t < nst ? sum : 0.f;
             split8(x, sca, f);
         }
     };
