@@ -31,8 +31,15 @@ constexpr int kTargetWG = NR_WGRAD_TARGET_WG;   // ~3 rounds of one workgroup pe
 #ifndef NR_WGRAD_TARGET_WG_GA
 #define NR_WGRAD_TARGET_WG_GA 1024
 #endif
-[[maybe_unused]] constexpr int kTargetWGMax = NR_WGRAD_TARGET_WG > NR_WGRAD_TARGET_WG_GA ? NR_WGRAD_TARGET_WG
-                                                                        : NR_WGRAD_TARGET_WG_GA;
+// the LDS-DMA kernel (wgrad4_kernel, one workgroup per CU) over a sample list:
+// 1536 measured 3% faster than 1024 (768: +0.5%, 2048: -1.5%) at cfg2's fine
+// pass (two alternating rounds, profiles/r05/ab/u_*)
+#ifndef NR_WGRAD_TARGET_WG_W4
+#define NR_WGRAD_TARGET_WG_W4 1536
+#endif
+constexpr int kMax2(int x, int y) { return x > y ? x : y; }
+[[maybe_unused]] constexpr int kTargetWGMax =
+    kMax2(kMax2(NR_WGRAD_TARGET_WG, NR_WGRAD_TARGET_WG_GA), NR_WGRAD_TARGET_WG_W4);
 constexpr int kThreads = 512;    // 8 waves: two per SIMD, so one wave's staging and
                                  // barrier time overlaps its partner's MFMAs
 constexpr int kCol = 36;         // LDS column stride (floats): [column][32 samples + 4 pad]
@@ -1497,14 +1504,6 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
             split8(x, sca, f);
         }
     };
-    auto split_b = [&](int t, int j, x3::Pieces& f) {
-        const float* pb = reinterpret_cast<const float*>(lds + (t % kD) * kSlot + kAImg + 8 * h * RSB) +
-                          32 * VB * wb + 32 * j + c;
-        float x[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] = pb[k * WB];
-        split8(x, 1.f, f);
-    };
     // wide form (VB > 1 / the gradient chunk): lane c holds rows 4c .. 4c + 3 of
     // its 128-row chunk (columns VB c .. VB c + VB - 1 of its column chunk), so
     // one ds_read_b128 (b64) per sample feeds 4 (VB) tiles: tile i holds rows
@@ -1933,7 +1932,15 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     // every launch over a sample list -- gathering (*_active) or over buffers
     // saved by position (*_listed, the deferred save) -- uses the same split-K
     // partition, so the two give bit-identical sums
-    const int64_t target_wg = slist ? NR_WGRAD_TARGET_WG_GA : kTargetWG;
+    // f16x3, full graph: the LDS-DMA weight gradient (wgrad4_kernel; NR_W4=0 at
+    // build time: the register-staged wgrad3_kernel).  32-bit buffer offsets:
+    // every segment it reads stays under 2 GiB below 2M samples.
+    // NR_WGRAD_W4=0 in the environment: the register-staged kernel, for A/B
+    // runs and the cross-check test (read per launch)
+    const char* w4_env = getenv("NR_WGRAD_W4");
+    const bool use_w4 = NR_F16 && NR_W4 && !sigma_only && n < ((int64_t)1 << 21) &&
+                        !(w4_env && atoi(w4_env) == 0);
+    const int64_t target_wg = !slist ? kTargetWG : (use_w4 ? NR_WGRAD_TARGET_WG_W4 : NR_WGRAD_TARGET_WG_GA);
     int64_t gt[kTasks];
     int pos[kTasks];
     for (int k = 0; k < kTasks; ++k) {
@@ -1955,14 +1962,6 @@ int wgrad_launch(bool x3, bool sigma_only, const float* save, const float* grad_
     // its gradient is W_dir[:, :256]^T G, nr_wgrad_dir_feat -- so the sigma
     // head pairs with task 10, which reads H(7) too)
     static const int kFused[2][2] = {{5, 4}, {10, 12}};   // {primary, partner}
-    // f16x3, full graph: the LDS-DMA weight gradient (wgrad4_kernel; NR_W4=0 at
-    // build time: the register-staged wgrad3_kernel)
-    // (32-bit buffer offsets: every segment it reads stays under 2 GiB below 2M samples)
-    // (NR_WGRAD_W4=0 in the environment: the register-staged kernel, for A/B
-    // runs and the cross-check test; read per launch)
-    const char* w4_env = getenv("NR_WGRAD_W4");
-    const bool use_w4 = NR_F16 && NR_W4 && !sigma_only && n < ((int64_t)1 << 21) &&
-                        !(w4_env && atoi(w4_env) == 0);
     static const bool fuse_on = !getenv("NR_WGRAD_FUSE") || atoi(getenv("NR_WGRAD_FUSE")) != 0;
     int partner[kTasks];
     bool absorbed[kTasks];

@@ -25,7 +25,7 @@ from ._lib import call, stream_of
 def _wgrad_workspace(device_index: int, stream: int = 0) -> torch.Tensor:
     """Split-K slab workspace of the weight gradient, one per (device, stream):
     backward passes enqueued on different streams never share slabs.  The
-    size is the library's bound over every launch shape (~604 MB; the slabs a
+    size is the library's bound over every launch shape (~1.2 GB; the slabs a
     launch uses depend only on the task list, not on n).  At most 4 are kept
     (least recently used evicted): a workspace is allocated while its stream is
     current, so once evicted the caching allocator hands its memory only to
