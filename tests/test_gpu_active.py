@@ -33,7 +33,7 @@ def _samples(g_out):
     return sl[:c].cpu().numpy(), c
 
 
-@pytest.mark.parametrize("n", [1, 31, 32, 33, 1000, 4096, 70001])
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 1000, 4096, 70001, 800017])
 def test_active_sample_list_matches_numpy(n):
     g = torch.Generator().manual_seed(n)
     x = torch.randn(n, 4, generator=g)
