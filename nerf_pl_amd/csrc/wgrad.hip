@@ -1301,8 +1301,11 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, int voff, int so
 __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* l) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr)l, 4, voff, soff, 0, 0);
 }
+// (the record count is an unsigned 32-bit byte count: at n just under 2^21 a
+// 256-wide gradient segment is exactly 2^31 bytes, past int's range)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0,
+                                             (int)(uint32_t)min(bytes, (int64_t)0xffffffff), 0x00020000);
 }
 template <int V> struct Vec { typedef float T __attribute__((ext_vector_type(V))); };
 template <> struct Vec<1> { typedef float T; };

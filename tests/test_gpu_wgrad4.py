@@ -64,3 +64,17 @@ def test_wgrad_dma_empty_list(monkeypatch):
     g = _grads(monkeypatch, True, True, "none", (23, 37), zero_frac=1.1)
     for k, v in g.items():
         assert (v == 0).all(), k
+
+
+def test_wgrad_dma_at_the_size_limit(monkeypatch):
+    """n = 2^21 - 1 (16,513 rays x 127 samples): the largest launch the LDS-DMA
+    kernel takes (wgrad_launch falls back at 2^21), where its 256-wide
+    gradient segments span exactly 2^31 bytes -- past int's range for the
+    buffer resources' record count; gathered list, every tensor against the
+    register-staged kernel."""
+    new = _grads(monkeypatch, True, True, "none", (16513, 127), zero_frac=0.45, seed=9)
+    old = _grads(monkeypatch, False, True, "none", (16513, 127), zero_frac=0.45, seed=9)
+    for k, ref in old.items():
+        scale = ref.abs().max().item()
+        err = (new[k] - ref).abs().max().item()
+        assert err <= RTOL * scale + 1e-30, f"{k}: {err:.3g} of {scale:.3g}"
