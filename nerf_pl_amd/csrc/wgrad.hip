@@ -1412,12 +1412,17 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
     // the uniform samples of this wave's one-row instructions of stage t (rows
     // wave * KB + k), from the index ring (one LDS read) or by position
     struct Rows { int s[KB > 0 ? KB : 1]; };
-    auto rows_of = [&](int t) {
+    // (the LDS read and the scalar take of them apart: rows_raw / rows_take)
+    auto rows_raw = [&](int t) {
+        int4 v{};
+        if constexpr (RPI == 1 && GA) v = *reinterpret_cast<const int4*>(idx_slot(t) + 16 * wave);
+        return v;
+    };
+    auto rows_take = [&](int t, const int4 v) {
         Rows r{};
         if constexpr (RPI == 1) {
             if constexpr (GA) {
                 static_assert(KB == 4, "one float4 of list entries per wave");
-                const int4 v = *reinterpret_cast<const int4*>(idx_slot(t) + 16 * wave);
                 r.s[0] = __builtin_amdgcn_readfirstlane(v.x);
                 r.s[1] = __builtin_amdgcn_readfirstlane(v.y);
                 r.s[2] = __builtin_amdgcn_readfirstlane(v.z);
@@ -1429,6 +1434,7 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
         }
         return r;
     };
+    auto rows_of = [&](int t) { return rows_take(t, rows_raw(t)); };
     // instruction k (< KV) of this wave's issue step for stage t
     auto issue_k = [&](int t, int k, const Rows& rw) {
         char* slot = lds + (t % kD) * kSlot;
@@ -1482,7 +1488,8 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
     for (int i = 0; i < TA; ++i)
 #pragma unroll
         for (int j = 0; j < VB; ++j) acc[i][j] = f32x16{};
-    float bs[4] = {0.f, 0.f, 0.f, 0.f}, hs = 0.f;
+    f32x4 bsv = {0.f, 0.f, 0.f, 0.f};
+    float hs = 0.f;
 
     // fragments of stage t: ds_read_b32 of one row / column and 8 samples per
     // lane (lanes c of a 32-lane half: 32 consecutive features, conflict-free
@@ -1503,7 +1510,7 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
             float sum = 0.f;
 #pragma unroll
             for (int k = 0; k < 8; ++k) { x[k] = pa[16 * k]; sum += x[k]; }
-            bs[i & 3] += t < nst ? sum : 0.f;
+            bsv[i & 3] += t < nst ? sum : 0.f;
             split8(x, sca, f);
         }
     };
@@ -1528,14 +1535,55 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
 #pragma unroll
         for (int k = 0; k < 8; ++k) r.v[k] = *reinterpret_cast<const BV*>(pb + k * RSB);
     };
+    // stage t's gradient rows, once per stage: their bias sums (the four row
+    // tiles at once, in packed fp32 pairs; wb == 0 writes them), then the rows
+    // times sca in place (packed too), so the splits below take them as they are
+    // (a stage's sums enter bsv one stage later, so those of stage nst -- the
+    // clamped read past the end -- never do, without a branch)
+    f32x4 bpend = {0.f, 0.f, 0.f, 0.f};
+    auto prep_sum = [&](const RawA& r) {
+        if constexpr (MA > 0) {
+            f32x4 sum = r.v[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) sum += r.v[k];
+            bsv += bpend;
+            bpend = sum;
+        }
+    };
+    auto prep_scale = [&](RawA& r) {
+        if constexpr (MA > 0)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r.v[k] *= sca;
+    };
+    auto prep_a = [&](int t, RawA& r) {
+        (void)t;
+        prep_sum(r);
+        prep_scale(r);
+    };
+    // the head tile (HD) of stage t: its 8 values (read) and its pieces (split)
+    auto read_h = [&](int t, float (&x)[8]) {
+        const float* ph = reinterpret_cast<const float*>(lds + (t % kD) * kSlot + kAImg + kBImg + 128 * h) +
+                          (c & 3);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float v = ph[4 * k];
+            x[k] = c < 4 ? v : 0.f;
+        }
+    };
+    auto split_h = [&](const float (&x)[8], x3::Pieces& f) {
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum += x[k];
+        hs += sum;
+        split8(x, sch, f);
+    };
     auto split_a_raw = [&](int t, const RawA& r, int i, x3::Pieces& f) {
         if (HD && i == HT) { split_a(t, i, f); return; }
         if constexpr (MA > 0) {
-            float x[8], sum = 0.f;
+            float x[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) { x[k] = r.v[k][i & 3]; sum += x[k]; }
-            if (wb == 0 && NR_W4_DBG != 4) bs[i & 3] += t < nst ? sum : 0.f;
-            split8(x, sca, f);
+            for (int k = 0; k < 8; ++k) x[k] = r.v[k][i & 3];
+            split8(x, 1.f, f);
         }
     };
     auto split_b_raw = [&](const RawB& r, int j, x3::Pieces& f) {
@@ -1560,23 +1608,29 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
         asm volatile("" ::: "memory");
         mask_tail(0);
         // pieces of the stage being multiplied: row tiles fa (each rewritten with
-        // the next stage's right after its MFMAs issued), column tiles fb (the
-        // next stage's go to fn first: every row tile still reads them)
+        // the next stage's right after its MFMAs issued), column tiles fb / fn
+        // (the next stage's go to the other set: every row tile still reads them)
         // every wave multiplies (a wave outside the grid reads in-bounds LDS
         // and writes nothing): no branch around the accumulators
-        x3::Pieces fa[TA], fb[VB];
+        x3::Pieces fa[TA], fb[VB], fn[VB];
+        // PH: the phased stage below (row tiles > 1, uniform input rows);
+        // else every split of stage s + 1 follows the row tile that frees it
+        constexpr bool PH = TA > 1 && RPI == 1;
+        RawA rA, rB;
+        int4 iv = rows_raw(kD);
         {
-            RawA r0;
             RawB q0;
-            read_a(0, r0);
+            read_a(0, rA);
             read_b(0, q0);
+            prep_a(0, rA);
 #pragma unroll
-            for (int i = 0; i < TA; ++i) split_a_raw(0, r0, i, fa[i]);
+            for (int i = 0; i < (PH ? TA - 1 : TA); ++i) split_a_raw(0, rA, i, fa[i]);
 #pragma unroll
             for (int j = 0; j < VB; ++j) split_b_raw(q0, j, fb[j]);
         }
-#pragma unroll 1
-        for (int s = 0; s < nst; ++s) {
+        // stage s: fa x cur, then stage s + 1 split into fa and nxt (the two
+        // column-piece sets trade roles from stage to stage: no copies)
+        auto stage = [&](int s, x3::Pieces (&cur)[VB], x3::Pieces (&nxt)[VB]) {
             // stage s + 1 landed (every wave's DMA) and stage s's slot is no longer read
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((kD - 2) * KV) : "memory");
             __builtin_amdgcn_s_barrier();
@@ -1585,7 +1639,6 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
             // stage s + kD's DMA goes out between this stage's MFMAs (its list
             // entries read first: one LDS read, used a row tile later)
             const Rows rw = rows_of(s + kD);
-            x3::Pieces fn[VB];
             RawA ra1;
             RawB rb1;
             if (NR_W4_DBG != 3) { read_a(s + 1, ra1); read_b(s + 1, rb1); }
@@ -1599,10 +1652,10 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
                 for (int p = 0; p < 3; ++p)
 #pragma unroll
                     for (int j = 0; j < VB; ++j) {
-                        if (NR_W4_DBG == 1) { asm volatile("" ::"v"(fa[i].lo), "v"(fa[i].hi), "v"(fb[j].lo), "v"(fb[j].hi)); continue; }
-                        acc[i][j] = p == 0 ? x3::mfma32(fa[i].lo, fb[j].hi, acc[i][j])
-                                  : p == 1 ? x3::mfma32(fa[i].hi, fb[j].lo, acc[i][j])
-                                           : x3::mfma32(fa[i].hi, fb[j].hi, acc[i][j]);
+                        if (NR_W4_DBG == 1) { asm volatile("" ::"v"(fa[i].lo), "v"(fa[i].hi), "v"(cur[j].lo), "v"(cur[j].hi)); continue; }
+                        acc[i][j] = p == 0 ? x3::mfma32(fa[i].lo, cur[j].hi, acc[i][j])
+                                  : p == 1 ? x3::mfma32(fa[i].hi, cur[j].lo, acc[i][j])
+                                           : x3::mfma32(fa[i].hi, cur[j].hi, acc[i][j]);
                         asm volatile("" : "+a"(acc[i][j]));   // accumulators stay in AGPRs
                     }
 #pragma unroll
@@ -1611,27 +1664,121 @@ __device__ __forceinline__ void wgrad4_body(const WgArgs& a, const WgTask& T, in
                 if (NR_W4_DBG == 3) continue;
                 if (i == 0) {
 #pragma unroll
-                    for (int j = 0; j < VB; ++j) split_b_raw(rb1, j, fn[j]);
+                    for (int j = 0; j < VB; ++j) split_b_raw(rb1, j, nxt[j]);
+                    prep_a(s + 1, ra1);
                 } else {
                     split_a_raw(s + 1, ra1, i - 1, fa[i - 1]);
                 }
             }
-            if (NR_W4_DBG == 3) continue;
+            if (NR_W4_DBG == 3) return;
             split_a_raw(s + 1, ra1, TA - 1, fa[TA - 1]);
+        };
+        // PH: stage s's reads (the head's values, then stage s + 1's input and
+        // gradient rows) all go out before the first MFMA, and the VALU work
+        // rides between the MFMAs, each piece after the MFMA that frees its
+        // registers and late enough that its reads have landed -- tile 0: the
+        // split of stage s's last row tile (deferred from stage s - 1: its raw
+        // values stay in registers; HD: the head tile); tile 1: stage s + 1's
+        // column tiles; tile 2: its bias sums, scaling and row tiles 0, 1; tile
+        // i > 2: row tile i - 1.  A sched_barrier before every MFMA fixes the
+        // interleave.  The next stage's list entries are read last (the
+        // top-of-stage wait covers that read).
+        auto stage_ph = [&](int s, x3::Pieces (&cur)[VB], x3::Pieces (&nxt)[VB], RawA& rc, RawA& rn) {
+            if constexpr (PH) {
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((kD - 2) * KV) : "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                mask_tail(s + 1);
+                const Rows rw = rows_take(s + kD, iv);
+                float xh[8];
+                if constexpr (HD) read_h(s, xh);
+                RawB rb1;
+                read_b(s + 1, rb1);
+                read_a(s + 1, rn);
+                // the VALU work after MFMA m of row tile i (NM per tile), each
+                // result pinned where it is made: later passes would otherwise
+                // sink it past the next stage's mask_tail branch
+                constexpr int NM = 3 * VB;
+                // (and its inputs pinned there too: the selector would hoist
+                // it above the MFMAs otherwise)
+                auto work = [&](int i, int m) {
+                    if (i == 0 && m == 0) {
+                        if constexpr (HD) {
 #pragma unroll
-            for (int j = 0; j < VB; ++j) fb[j] = fn[j];
+                            for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(xh[k]));
+                            split_h(xh, fa[TA - 1]);
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(rc.v[k]));
+                            split_a_raw(s, rc, TA - 1, fa[TA - 1]);
+                        }
+                        x3::pin(fa[TA - 1]);
+                    } else if (i == 1 && m % 3 == 0) {
+                        if (m == 0)
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(rb1.v[k]));
+                        split_b_raw(rb1, m / 3, nxt[m / 3]);
+                        x3::pin(nxt[m / 3]);
+                    } else if (i == 2 && m == 0) {
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(rn.v[k]));
+                        prep_sum(rn);
+                        asm volatile("" : "+v"(bsv), "+v"(bpend));
+                    } else if (i == 2 && m == 1) {
+                        prep_scale(rn);
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(rn.v[k]));
+                    } else if (i == 2 && (m == NM / 3 || m == 2 * NM / 3)) {
+                        const int t = m == NM / 3 ? 0 : 1;
+                        split_a_raw(s + 1, rn, t, fa[t]);
+                        x3::pin(fa[t]);
+                    } else if (i > 2 && m == 0) {
+                        split_a_raw(s + 1, rn, i - 1, fa[i - 1]);
+                        x3::pin(fa[i - 1]);
+                    }
+                    if (m == 1)
+#pragma unroll
+                        for (int k = i * KV / TA; k < (i + 1) * KV / TA; ++k) issue_k(s + kD, k, rw);
+                    if (i == TA - 1 && m == NM - 1) iv = rows_raw(s + 1 + kD);
+                };
+#pragma unroll
+                for (int i = 0; i < TA; ++i)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+#pragma unroll
+                        for (int j = 0; j < VB; ++j) {
+                            __builtin_amdgcn_sched_barrier(0);
+                            acc[i][j] = p == 0 ? x3::mfma32(fa[i].lo, cur[j].hi, acc[i][j])
+                                      : p == 1 ? x3::mfma32(fa[i].hi, cur[j].lo, acc[i][j])
+                                               : x3::mfma32(fa[i].hi, cur[j].hi, acc[i][j]);
+                            asm volatile("" : "+a"(acc[i][j]));
+                            work(i, p * VB + j);
+                        }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        // (nst is even: two stages per 32-sample block)
+#pragma unroll 1
+        for (int s = 0; s < nst; s += 2) {
+            if constexpr (PH) {
+                stage_ph(s, fb, fn, rA, rB);
+                stage_ph(s + 1, fn, fb, rB, rA);
+            } else {
+                stage(s, fb, fn);
+                stage(s + 1, fn, fb);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped DMAs past the end
     }
     if (!active) return;
     // bias sums: lanes c (h = 0, 1: samples 0..7, 8..15 of each stage)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bs[i] += __shfl_xor(bs[i], 32);
+    for (int i = 0; i < 4; ++i) bsv[i] += __shfl_xor(bsv[i], 32);
     hs += __shfl_xor(hs, 32);
     if (wb == 0 && h == 0) {
         if constexpr (MA > 0) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) slab[MA * WB + 128 * wa + 4 * c + i] = bs[i];
+            for (int i = 0; i < 4; ++i) slab[MA * WB + 128 * wa + 4 * c + i] = bsv[i];
         }
         if constexpr (HD) if (c < 4) hslab[4 * WB + c] = hs;
     }
