@@ -50,10 +50,12 @@ struct GScale {
     float mx[2] = {0.f, 0.f};    // max |B value| seen by this lane, per sample tile
 };
 
-// max over the 4 lane groups (the features of a sample)
-__device__ __forceinline__ float max_over_groups(float m) {
-    m = fmaxf(m, __shfl_xor(m, 16));
-    return fmaxf(m, __shfl_xor(m, 32));
+// (max_over_groups, x3.h: max over the 4 lane groups = the features of a sample)
+
+// 1 / sig for a power of two sig in [2^-126, 2^126] (every sigma here: |log2| <=
+// kSigLim), exact, so x * inv_pow2(sig) == x / sig bit for bit
+__device__ __forceinline__ float inv_pow2(float sig) {
+    return __uint_as_float(0x7f000000u - __float_as_uint(sig));
 }
 
 // renormalise after a producer: see GScale; inj = bound of the values injected
@@ -70,15 +72,14 @@ __device__ __forceinline__ void gscale_from(GScale& sc, const GScale& prod, cons
         f = __uint_as_float((uint32_t)(127 + en - es) << 23);
         sc.sig[S] = prod.sig[S] * f;
         sc.ks[S] = f * kWUnscale;
-        sc.kst[S] = kWUnscale / prod.sig[S];
+        sc.kst[S] = kWUnscale * inv_pow2(prod.sig[S]);
     }
 }
 
 // max |true gradient| of a segment over the wave -> its per-wave slot
 // (layout.h NR_STAT_SEGS; reduced by wgrad.hip)
 __device__ __forceinline__ void report_max(float m, float* slot, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+    m = wave_max(m);
     if (lane == 0) *slot = m;
 }
 
@@ -133,7 +134,7 @@ struct GradU {
     // after the last split: the segment's max |true value| -> its stats slot
     __device__ __forceinline__ void report(float* slot) const {
         if constexpr (NR_F16)
-            report_max(fmaxf(sc.mx[0] / sc.sig[0], sc.mx[1] / sc.sig[1]), slot, lane);
+            report_max(fmaxf(sc.mx[0] * inv_pow2(sc.sig[0]), sc.mx[1] * inv_pow2(sc.sig[1])), slot, lane);
     }
 };
 
@@ -444,7 +445,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_bwd3_kernel(Bwd3Args a) {
         mwords(0, mw);
         float* d1 = dzseg(0);
         float m1 = 0.f;
-        const float k1[2] = {kWUnscale / u2.sc.sig[0], kWUnscale / u2.sc.sig[1]};
+        const float k1[2] = {kWUnscale * inv_pow2(u2.sc.sig[0]), kWUnscale * inv_pow2(u2.sc.sig[1])};
 #pragma unroll
         for (int F = 0; F < 16; ++F)
 #pragma unroll

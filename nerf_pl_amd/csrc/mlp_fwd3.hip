@@ -69,10 +69,7 @@ __device__ __forceinline__ void head_dot(const f32x4 (&acc)[NF][2], const float*
             for (int r = 0; r < 4; ++r) p[S] = fmaf(RELU ? relu_i(acc[F][S][r]) : acc[F][S][r], v[r], p[S]);
     }
 #pragma unroll
-    for (int S = 0; S < 2; ++S) {
-        p[S] += __shfl_xor(p[S], 16);
-        p[S] += __shfl_xor(p[S], 32);
-    }
+    for (int S = 0; S < 2; ++S) p[S] = sum_over_groups(p[S]);
 }
 
 // xyz positional encoding in the slot order of packing.PE16_MAP: lane group g
@@ -490,10 +487,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         float sigma[2];
 #pragma unroll
         for (int S = 0; S < 2; ++S) {
-            float p = u8.sig[S];
-            p += __shfl_xor(p, 16);
-            p += __shfl_xor(p, 32);
-            sigma[S] = p + H[NR_H_BSIG];
+            sigma[S] = sum_over_groups(u8.sig[S]) + H[NR_H_BSIG];
         }
         if (wr && !LIST)
             *reinterpret_cast<f32x4*>(a.out + (size_t)sw * 4) = f32x4{0.f, 0.f, 0.f, Sw ? sigma[1] : sigma[0]};
@@ -537,10 +531,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         float sigma[2];
 #pragma unroll
         for (int S = 0; S < 2; ++S) {
-            float p = u8.sig[S];
-            p += __shfl_xor(p, 16);
-            p += __shfl_xor(p, 32);
-            sigma[S] = p + H[NR_H_BSIG];
+            sigma[S] = sum_over_groups(u8.sig[S]) + H[NR_H_BSIG];
         }
         f32x4 C[8][2];
         { auto bi = bias(NR_H_BDIR); segment<FwdTab, kDir, 8, 1, QEND, true>(dma, lane, C, uf, dpeu, bi, none, b, f0); }

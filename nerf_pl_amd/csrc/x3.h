@@ -330,6 +330,52 @@ __device__ __forceinline__ void pin(Pieces& p) {
 #endif
 }
 
+// Lane-pair exchanges without an LDS round trip (__shfl_xor goes through
+// ds_bpermute: ~100 cycles of latency each, exposed at one wave per SIMD).
+// v_permlane16_swap (v_permlane32_swap) of x with itself leaves lanes l and
+// l ^ 16 (l ^ 32) holding the pair {x[l], x[l ^ 16]} split across the two
+// results, so for a commutative op, op(r0, r1) == op(x[l], x[l ^ 16]) in
+// every lane -- bit for bit the __shfl_xor form (IEEE + and max commute).
+__device__ __forceinline__ void pair16(float x, float& r0, float& r1) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    r0 = __uint_as_float(r[0]);
+    r1 = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void pair32(float x, float& r0, float& r1) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    r0 = __uint_as_float(r[0]);
+    r1 = __uint_as_float(r[1]);
+}
+// x[l] + x[l ^ 16] + x[l ^ 32] + x[l ^ 48] in the __shfl_xor order (16, then 32)
+__device__ __forceinline__ float sum_over_groups(float x) {
+    float a, b;
+    pair16(x, a, b);
+    x = a + b;
+    pair32(x, a, b);
+    return a + b;
+}
+// max over the 4 lane groups of 16 (l, l ^ 16, l ^ 32, l ^ 48)
+__device__ __forceinline__ float max_over_groups(float x) {
+    float a, b;
+    pair16(x, a, b);
+    x = fmaxf(a, b);
+    pair32(x, a, b);
+    return fmaxf(a, b);
+}
+// max over the wave, in every lane: DPP within rows of 16 (quad xor 1, xor 2,
+// half-row mirror, row mirror), then the two swaps (max is order-free)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_max(float x) {
+    x = fmaxf(x, dpp_f<0xB1>(x));     // quad_perm [1,0,3,2]
+    x = fmaxf(x, dpp_f<0x4E>(x));     // quad_perm [2,3,0,1]
+    x = fmaxf(x, dpp_f<0x141>(x));    // row_half_mirror
+    x = fmaxf(x, dpp_f<0x140>(x));    // row_mirror
+    return max_over_groups(x);
+}
+
 // ReLU as an integer max: negative floats (and -0) have the sign bit set
 __device__ __forceinline__ float relu_i(float x) {
     return __int_as_float(max(__float_as_int(x), 0));
