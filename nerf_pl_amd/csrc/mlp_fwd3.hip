@@ -225,6 +225,18 @@ struct AccU {
     f32x4 held = {0.f, 0.f, 0.f, 0.f};   // kPaired: the even tile, stored with the odd one
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     float sig[2] = {0.f, 0.f};
+    // SIG: the sigma weights of k-step s (features kmap16(s, g, 2p) and +1)
+    // are read one k-step ahead, into wsg[s & 1], so no LDS read is waited on
+    // right where it is used; preload() reads k-step 0's a segment early
+    f32x2 wsg[2][4];
+    __device__ __forceinline__ f32x2 wsig_of(int s, int p) const {
+        return *reinterpret_cast<const f32x2*>(wsig + 32 * s + 16 * (p >> 1) + 4 * g + 2 * (p & 1));
+    }
+    __device__ __forceinline__ void preload() {
+        if constexpr (SIG)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) wsg[0][p] = wsig_of(0, p);
+    }
     template <typename SC>
     __device__ __forceinline__ void operator()(SC, int sb, int p, float& x0, float& x1) {
         constexpr int s = SC::value;
@@ -233,8 +245,10 @@ struct AccU {
         if constexpr (RELU) { x0 = relu_i(x0); x1 = relu_i(x1); }
         if constexpr (kWScale != 0) { x0 *= kWUnscale; x1 *= kWUnscale; }   // exact
         if constexpr (SIG) {
-            // feature kmap16(s, g, 2p) and +1
-            const f32x2 wv = *reinterpret_cast<const f32x2*>(wsig + 32 * s + 16 * (p >> 1) + 4 * g + 2 * (p & 1));
+            // (units run s-major, sb = 0 before 1: wsg[(s + 1) & 1][p] was
+            // last read by unit (s - 1, 1, p))
+            if (sb == 0 && s + 1 < 8) wsg[(s + 1) & 1][p] = wsig_of(s + 1, p);
+            const f32x2 wv = wsg[s & 1][p];
             sig[sb] = fmaf(x0, wv[0], sig[sb]);
             sig[sb] = fmaf(x1, wv[1], sig[sb]);
         }
@@ -483,6 +497,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         // sums; out rows are (n, 4) [0, 0, 0, sigma] for the backward's contract
         { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, nonext, bi, none, b, f0); }
         AccU<true, true, true, true, false> u8{B, hseg(7), mseg(7), H + NR_H_WSIG, lane, g};
+        u8.preload();
         drain_all(u8);
         float sigma[2];
 #pragma unroll
@@ -501,6 +516,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     } else {
         // h8 feeds xyz_encoding_final and, while it is split, the sigma head
         AccU<true, SAVE, SAVE, true> u8{B, hseg(7), mseg(7), H + NR_H_WSIG, lane, g};
+        u8.preload();
         { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, u8, bi, none, b, f0); }
         NR_STAMP(10);
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
