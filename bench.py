@@ -835,7 +835,7 @@ def main():
         roof, roofs, stage = None, {}, None
         if ks:
             tj = {}
-            for rel in ("profiles/r05/traffic.json", "profiles/r04/traffic.json", "profiles/r03/traffic.json",
+            for rel in ("profiles/r05/late/traffic.json", "profiles/r05/traffic.json", "profiles/r04/traffic.json", "profiles/r03/traffic.json",
                         "profiles/r02/traffic.json",
                         "profiles/r01/traffic.json"):
                 tf = os.path.join(REPO, rel)

@@ -61,7 +61,7 @@ for k in sorted(fetch):
     fb, wb = fetch[k][0] * 1024 * 2, write[k][0] * 1024
     res[k] = {"samples": 786432, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
               "launches": fetch[k][1], "arithmetic": k.split("/")[0],
-              "file": "profiles/r05/traffic.json",
+              "file": out,
               "method": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over bench.py's "
                         "short cfg2 run (fine-pass launches: the largest grid; backward on the samples "
                         "with a nonzero output gradient); FETCH_SIZE x2 (gfx950 wide-stream correction)"}
