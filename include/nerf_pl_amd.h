@@ -33,7 +33,10 @@ const char* nr_last_error(void);
 
 /* Layout constants shared with the Python packer (0: forward packed floats,
  * 1: head offset, 2: backward packed floats, 3: saved floats/sample,
- * 4: gradient floats/sample, 5: head floats, 6..8: layer offsets). */
+ * 4: gradient floats/sample, 5: head floats, 6..8: layer offsets) and
+ * 9: the ABI revision -- 2 since full-graph nr_wgrad* launches leave G in
+ * dir_encoding.0.weight[:, :256] for nr_wgrad_dir_feat to finish (see
+ * nr_wgrad below); a caller built against revision 1 must refuse it. */
 int64_t nr_layout_query(int what);
 
 /* Gather the flat parameter buffer (595,844 floats, NeRF.named_parameters()

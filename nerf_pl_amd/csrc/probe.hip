@@ -13,6 +13,10 @@ NR_API int64_t nr_layout_query(int what) {
         case 6: return NR_F_L5;
         case 7: return NR_F_DIR;
         case 8: return NR_B_L5T;
+        // ABI revision: 2 = a full-graph nr_wgrad* launch leaves G = sum dz_dir h8^T
+        // in dir_encoding.0.weight[:, :256] and zeros in xyz_encoding_final, and
+        // nr_wgrad_dir_feat must follow it (round 5; 1 = every gradient final)
+        case 9: return 2;
         default: return -1;
     }
 }

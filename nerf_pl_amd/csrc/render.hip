@@ -18,7 +18,8 @@ __device__ __forceinline__ double wave_incl_prod(double v, int lane) {
     return v;
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
     return v;
@@ -26,13 +27,14 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 // Reverse (suffix) scan of affine maps R -> a*R + b, composed right-to-left:
 // returns for lane i the composition f_i o f_{i+1} o ... o f_63 as (A, B).
-__device__ __forceinline__ void wave_suffix_affine(float& a, float& b, int lane) {
+template <typename T>
+__device__ __forceinline__ void wave_suffix_affine(T& a, T& b, int lane) {
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const float na = __shfl_down(a, d);
-        const float nb = __shfl_down(b, d);
+        const T na = __shfl_down(a, d);
+        const T nb = __shfl_down(b, d);
         if (lane + d < 64) {   // f_i o g: R -> a*(na*R + nb) + b
-            b = fmaf(a, nb, b);
+            b = fma(a, nb, b);
             a = a * na;
         }
     }
@@ -113,7 +115,13 @@ __global__ void composite_fwd_kernel(CompArgs a) {
     const int S = a.S;
     const int64_t base = (int64_t)ray * S;
     double carry = 1.0;
-    float acc_w = 0.f, acc_r = 0.f, acc_g = 0.f, acc_b = 0.f, acc_d = 0.f;
+    float acc_w = 0.f, acc_r = 0.f, acc_g = 0.f, acc_b = 0.f;
+    // depth = sum w_i z_i (rendering.py:185) in double: at near/far 1/200 the
+    // terms reach ~200, where an fp32 sum over 192 samples drifts by ~3e-5 --
+    // a third of the north star's 1e-4 abs.  In double our depth is the exact
+    // sum of the fp32 products rounded once, so its distance from the
+    // reference is the reference's own (fp32) summation error
+    double acc_d = 0.0;
     for (int c0 = 0; c0 < S; c0 += 64) {
         const int i = c0 + lane;
         const bool v = i < S;
@@ -145,7 +153,7 @@ __global__ void composite_fwd_kernel(CompArgs a) {
                     acc_g = fmaf(w, rr[1], acc_g);
                     acc_b = fmaf(w, rr[2], acc_b);
                 }
-                acc_d = fmaf(w, zi, acc_d);
+                acc_d = fma((double)w, (double)zi, acc_d);
             }
         }
     }
@@ -163,7 +171,7 @@ __global__ void composite_fwd_kernel(CompArgs a) {
             a.rgb[(size_t)ray * 3 + 1] = acc_g + bg;
             a.rgb[(size_t)ray * 3 + 2] = acc_b + bg;
         }
-        a.depth[ray] = acc_d;
+        a.depth[ray] = (float)acc_d;
         a.opacity[ray] = acc_w;
     }
 }
@@ -175,6 +183,13 @@ __global__ void composite_fwd_kernel(CompArgs a) {
 //   da_i  = T_i (dw_i - R_i)
 //   dsig  = da_i * exp(-delta r) * delta * [sigma + n > 0]
 //   dc_i  = w_i * drgb
+// Evaluated in double from the fp32 inputs (sigma + noise as the forward
+// rounds it, depths, directions), each gradient rounded to fp32 once:
+// dw_i - R_i cancels (a sample's own colour against the transmittance-weighted
+// colours behind it), and in fp32 that cancellation made d sigma -- and the
+// sigma bias's gradient, a sum of d sigma over every sample -- the one
+// gradient measurably farther from float64 than the reference's fp32
+// autograd (tests/test_gpu_cfg4.py at near/far 1/200)
 // ---------------------------------------------------------------------------
 struct CompBwdArgs {
     const float* raw; int raw_stride; int sig_col; const float* z; const float* rays; const float* noise;
@@ -184,77 +199,82 @@ struct CompBwdArgs {
     float* g_raw;   // (n_rays*S, raw_stride)
 };
 
+// delta_i in double from the fp32 depths (the last: 1e10 |d|, rendering.py:171)
+__device__ __forceinline__ double delta_d(const float* z, int64_t base, int i, int S, double dn) {
+    if (i + 1 < S) return ((double)z[base + i + 1] - (double)z[base + i]) * dn;
+    return S > 1 ? 1e10 * dn : 0.0;
+}
+
 __global__ void composite_bwd_kernel(CompBwdArgs a) {
     const int lane = threadIdx.x & 63;
     const int ray = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (ray >= a.n_rays) return;
     const float* r = a.rays + (size_t)ray * 8;
-    const float dn = ray_dnorm(r);
+    const double dn = sqrt((double)r[3] * r[3] + (double)r[4] * r[4] + (double)r[5] * r[5]);
     const int S = a.S;
     const int64_t base = (int64_t)ray * S;
     const float gr = a.g_rgb ? a.g_rgb[(size_t)ray * 3 + 0] : 0.f;
     const float gg = a.g_rgb ? a.g_rgb[(size_t)ray * 3 + 1] : 0.f;
     const float gb = a.g_rgb ? a.g_rgb[(size_t)ray * 3 + 2] : 0.f;
     const float gd = a.g_depth ? a.g_depth[ray] : 0.f;
-    float go = a.g_opacity ? a.g_opacity[ray] : 0.f;
-    if (a.white_back) go -= (gr + gg + gb);
+    double go = a.g_opacity ? a.g_opacity[ray] : 0.f;
+    if (a.white_back) go -= (double)gr + (double)gg + (double)gb;
     const int nchunks = (S + 63) >> 6;
+    // relu(sigma + noise) as the forward forms it (fp32 add), widened
+    auto rel = [&](int i) {
+        const float s = nr_add(a.raw[(base + i) * a.raw_stride + a.sig_col],
+                               sample_noise(a.noise, a.noise_std, a.seed, a.stream, base + i));
+        return s;
+    };
 
     // pass 1: forward transmittance carry per chunk start, kept implicitly by
     // recomputation; pass 2 walks chunks from the back carrying R.
-    float Rcarry = 0.f;   // R at the first sample of the following chunk, seen from before it
+    double Rcarry = 0.0;  // R at the first sample of the following chunk, seen from before it
     for (int ci = nchunks - 1; ci >= 0; --ci) {
         const int c0 = ci * 64;
         // transmittance entering this chunk
         double carry = 1.0;
         for (int cj = 0; cj < ci; ++cj) {
             const int j = cj * 64 + lane;
-            float fac = 1.f;
+            double fac = 1.0;
             if (j < S) {
-                const float zj = a.z[base + j];
-                const float delta = j + 1 < S ? nr_mul(nr_sub(a.z[base + j + 1], zj), dn)
-                                              : last_delta(S, dn);
-                const float al = alpha_of(a.raw[(base + j) * a.raw_stride + a.sig_col],
-                                          sample_noise(a.noise, a.noise_std, a.seed, a.stream,
-                                                       base + j), delta);
-                fac = nr_add(1.f - al, 1e-10f);
+                const float s = rel(j);
+                fac = exp(-delta_d(a.z, base, j, S, dn) * (s > 0.f ? (double)s : 0.0)) + 1e-10;
             }
-            carry *= __shfl(wave_incl_prod((double)fac, lane), 63);
+            carry *= __shfl(wave_incl_prod(fac, lane), 63);
         }
         const int i = c0 + lane;
         const bool v = i < S;
-        float alpha = 0.f, zi = 0.f, delta = 0.f, srel = 0.f, cr = 0.f, cg = 0.f, cb = 0.f;
+        double alpha = 0.0, e = 1.0, delta = 0.0;
+        float srel = 0.f, cr = 0.f, cg = 0.f, cb = 0.f, zi = 0.f;
         if (v) {
             zi = a.z[base + i];
-            delta = i + 1 < S ? nr_mul(nr_sub(a.z[base + i + 1], zi), dn) : last_delta(S, dn);
+            delta = delta_d(a.z, base, i, S, dn);
             const float* rr = a.raw + (base + i) * a.raw_stride;
             if (a.raw_stride == 4) { cr = rr[0]; cg = rr[1]; cb = rr[2]; }
-            const float sg = rr[a.sig_col];
-            const float nz = sample_noise(a.noise, a.noise_std, a.seed, a.stream, base + i);
-            srel = nr_add(sg, nz);
-            alpha = alpha_of(sg, nz, delta);
+            srel = rel(i);
+            e = exp(-delta * (srel > 0.f ? (double)srel : 0.0));
+            alpha = 1.0 - e;
         }
-        const float fac = v ? nr_add(1.f - alpha, 1e-10f) : 1.f;
-        const double incl = wave_incl_prod((double)fac, lane);
+        const double fac = v ? e + 1e-10 : 1.0;       // 1 - alpha + 1e-10
+        const double incl = wave_incl_prod(fac, lane);
         double excl = __shfl_up(incl, 1);
         if (lane == 0) excl = 1.0;
-        const float T = (float)(carry * excl);
-        const float w = nr_mul(alpha, T);
-        float dw = 0.f;
-        if (v) dw = fmaf(gr, cr, fmaf(gg, cg, fmaf(gb, cb, fmaf(gd, zi, go))));
+        const double T = carry * excl;
+        double dw = 0.0;
+        if (v) dw = (double)gr * cr + (double)gg * cg + (double)gb * cb + (double)gd * zi + go;
         // suffix affine scan inside the chunk: element i contributes the map
         // R -> f_i R + dw_i a_i to the samples before it.
-        float A = v ? fac : 1.f, Bv = v ? dw * alpha : 0.f;
+        double A = fac, Bv = v ? dw * alpha : 0.0;
         wave_suffix_affine(A, Bv, lane);   // lane i: composition f_i..f_63
         // R_i = composition of lanes i+1..63 applied to Rcarry
-        float An = __shfl_down(A, 1), Bn = __shfl_down(Bv, 1);
-        if (lane == 63) { An = 1.f; Bn = 0.f; }
-        const float Ri = fmaf(An, Rcarry, Bn);
-        const float Rnext = fmaf(__shfl(A, 0), Rcarry, __shfl(Bv, 0));
+        double An = __shfl_down(A, 1), Bn = __shfl_down(Bv, 1);
+        if (lane == 63) { An = 1.0; Bn = 0.0; }
+        const double Ri = fma(An, Rcarry, Bn);
+        const double Rnext = fma(__shfl(A, 0), Rcarry, __shfl(Bv, 0));
         if (v) {
-            const float da = T * (dw - Ri);
-            const float rl = srel > 0.f ? srel : 0.f;
-            const float dsig = srel > 0.f ? da * expf(nr_mul(-delta, rl)) * delta : 0.f;
+            const float dsig = srel > 0.f ? (float)(T * (dw - Ri) * e * delta) : 0.f;
+            const float w = (float)(alpha * T);
             if (a.raw_stride == 4) {
                 f32x4 o = {w * gr, w * gg, w * gb, dsig};
                 *reinterpret_cast<f32x4*>(a.g_raw + (base + i) * 4) = o;

@@ -123,7 +123,8 @@ def _note_listed(model, sigma_only, count_dev, n):
 # buffer, index of its length) to, so the rooflines count the samples worked on
 ACTIVE_LOG = None
 
-# NERF_PL_AMD_DEBUG=1 keeps the last backward's buffers here (dev/ scripts)
+# NERF_PL_AMD_DEBUG=1 keeps the last backward's buffers here (dev/ scripts;
+# tests set it to {} for one call) and every training forward's save buffer
 _DEBUG = {} if os.environ.get("NERF_PL_AMD_DEBUG") == "1" else None
 
 _SHAPES = list(packing.param_shapes().items())
@@ -161,17 +162,26 @@ class _FusedMLP(torch.autograd.Function):
             z = ops._dev(z, "z")
         out, save = ops.mlp_forward(packed_f, rays=rays, z=z, samples_per_ray=spr, x=x,
                                     sigma_only=kern_sigma_only, save=train and not defer)
+        if _DEBUG is not None and save is not None:
+            # the training forward's saved activations, in call order (tests
+            # read the ReLU masks the kernels chose: tests/grad64.py mlp_flips)
+            _DEBUG.setdefault("fwd_saves", []).append((save, out.shape[0], ops.MATH))
         if train:
+            # the flat parameters the forward ran with (the dir layer's
+            # feat-column weight gradient reads W_final, b_final and W_dir
+            # there: nr_wgrad_dir_feat), and the parameters themselves, so that
+            # autograd's version check raises if one changes in place between
+            # this forward and its backward, as it would for the reference's
+            # nn.Linear graph (a parameter's storage is a view of
+            # flat, but its version counter is its own)
+            flat = model.flat_params()
             if defer:     # the backward recomputes the listed samples' activations
-                ctx.save_for_backward(out, rays, z, packed_f, packed_b)
+                ctx.save_for_backward(out, rays, z, packed_f, packed_b, flat, *params)
                 ctx.spr = spr
             else:
-                ctx.save_for_backward(out, save, packed_f, packed_b)
+                ctx.save_for_backward(out, save, packed_f, packed_b, flat, *params)
             ctx.defer = defer
             ctx.sigma_only = sigma_only
-            # the flat parameters the forward ran with (the dir layer's
-            # feat-column weight gradient needs W_final, b_final: nr_wgrad_dir_feat)
-            ctx.flat = model.flat_params()
             ctx.model = model if DEFER_SAVE == "auto" else None
             ctx.so_kernels = so_train
         if sigma_only and train and out.shape[1] == 4:
@@ -182,7 +192,7 @@ class _FusedMLP(torch.autograd.Function):
     def backward(ctx, g_out):
         if ctx.defer:
             return _FusedMLP._backward_deferred(ctx, g_out)
-        out, save, packed_f, packed_b = ctx.saved_tensors
+        out, save, packed_f, packed_b, flat = ctx.saved_tensors[:5]
         n = out.shape[0]
         dev = out.device
         if ctx.sigma_only:
@@ -213,7 +223,7 @@ class _FusedMLP(torch.autograd.Function):
         call(ops.entry("nr_wgrad" + sfx, packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
              ws.data_ptr(), gflat.data_ptr(), *active, st)
         if not ctx.so_kernels:
-            _dir_feat(ctx, gflat, st)
+            _dir_feat(flat, gflat, st)
         if _DEBUG is not None:
             _DEBUG.update(save=save, grad_ws=grad_ws, g_out=g_out, gflat=gflat, n=n)
             _DEBUG.setdefault("g_outs", []).append(g_out)
@@ -224,7 +234,7 @@ class _FusedMLP(torch.autograd.Function):
         """The deferred save's backward: the sample list of g_out, the training
         forward re-run over the listed samples (activations saved by position),
         then the data and weight gradients over those positions."""
-        out, rays, z, packed_f, packed_b = ctx.saved_tensors
+        out, rays, z, packed_f, packed_b, flat = ctx.saved_tensors[:6]
         n = z.numel()
         dev = z.device
         if g_out.shape[1] == 1:            # a sigma-only graph's d sigma
@@ -256,14 +266,14 @@ class _FusedMLP(torch.autograd.Function):
         call(ops.entry("nr_wgrad" + sfx, packed_b), save.data_ptr(), grad_ws.data_ptr(), n,
              ws.data_ptr(), gflat.data_ptr(), *lst, st)
         if not so:
-            _dir_feat(ctx, gflat, st)
+            _dir_feat(flat, gflat, st)
         return (None,) * 6 + _param_grads(gflat, ctx.sigma_only)
 
 
-def _dir_feat(ctx, gflat, st):
+def _dir_feat(flat, gflat, st):
     """dir_encoding.0.weight's feat columns: the weight-gradient launch leaves
     G = sum dz_dir h8^T there (feat is not saved); G W_final^T + db b_final^T"""
-    call("nr_wgrad_dir_feat", ctx.flat.data_ptr(), gflat.data_ptr(), st)
+    call("nr_wgrad_dir_feat", flat.data_ptr(), gflat.data_ptr(), st)
 
 
 def _param_grads(gflat, sigma_only):

@@ -40,17 +40,23 @@ SAVE_STATS, STAT_SEGS = 16, 11
 
 
 _LAYOUT_OK = False
+# nr_layout_query(9): 2 = full-graph nr_wgrad* leave G for nr_wgrad_dir_feat
+ABI_REVISION = 2
 
 
 def _check_layout():
-    """The library's save / gradient block sizes must be this module's: a
-    library built from other sources would write past buffers sized here"""
+    """The library's save / gradient block sizes and ABI revision must be this
+    module's: a library built from other sources would write past buffers
+    sized here (the round-5 abort, tests/test_layout_guard.py) or leave
+    gradients this module does not finish"""
     global _LAYOUT_OK
     if not _LAYOUT_OK:
-        got = (int(lib().nr_layout_query(3)), int(lib().nr_layout_query(4)))
-        if got != (SAVE_PER_BLOCK, GRAD_PER_BLOCK):
-            raise RuntimeError(f"nerf_pl_amd: libnerf_pl_amd.so has save/grad blocks {got}, the package "
-                               f"{(SAVE_PER_BLOCK, GRAD_PER_BLOCK)}: rebuild the library (make)")
+        q = lib().nr_layout_query
+        got = (int(q(3)), int(q(4)), int(q(9)))
+        want = (SAVE_PER_BLOCK, GRAD_PER_BLOCK, ABI_REVISION)
+        if got != want:
+            raise RuntimeError(f"nerf_pl_amd: libnerf_pl_amd.so has (save block, grad block, ABI "
+                               f"revision) {got}, the package {want}: rebuild the library (make)")
         _LAYOUT_OK = True
 
 

@@ -130,19 +130,20 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
         result["depth_coarse"] = depth_c
         result["opacity_coarse"] = opac_c
 
+    cap["weights_coarse"] = w_c
     if N_importance > 0:
         # sample_pdf + sort(cat[z, z_pdf]) (rendering.py:253-257), weights detached
         u = rng.rand((n_rays, N_importance), dev)
         jit = rng.rand((n_rays, N_importance), dev)
         _, z_f = ops.sample_pdf(w_c.detach(), rays, N_importance, u=u, jitter=jit, seed=seed,
                                 z_coarse=z_c, merge=True)
-        cap["weights_coarse"] = w_c
         cap["z_fine"] = z_f
         s_f = N_samples + N_importance
         noise_f = rng.randn((n_rays, s_f), dev)
         raw_f = mlp(models[1], z_f, s_f)
-        rgb_f, depth_f, opac_f, _ = composite_apply(raw_f, z_f, rays, noise_f, noise_std, seed,
-                                                    STREAM_NOISE_FINE, white_back)
+        rgb_f, depth_f, opac_f, w_f = composite_apply(raw_f, z_f, rays, noise_f, noise_std, seed,
+                                                      STREAM_NOISE_FINE, white_back)
+        cap["weights_fine"] = w_f
         result["rgb_fine"] = rgb_f
         result["depth_fine"] = depth_f
         result["opacity_fine"] = opac_f

@@ -9,9 +9,9 @@ reference by tests/golden) with the reference's random draws replayed:
 
 * the rays themselves against the host restatement of get_ray_directions /
   get_rays (datasets/ray_utils.py) at 2e-6;
-* render_rays' every output at 1e-4 (depths relative), coarse weights at
-  1e-4, every ray whose fine depths moved explained by a sample_pdf knot flip
-  (tests/screening.py);
+* render_rays' every output and both passes' weights at 1e-4 ABSOLUTE
+  (tests/parity.py; depths reach ~200 at near/far 1/200), every ray whose
+  fine depths moved explained by a sample_pdf knot flip (tests/screening.py);
 * the training step's parameter gradients (MSE coarse + fine against the
   batch's target colours, train.py:107) on a 1,024-ray share of the batch,
   against the float64 oracle: within max(1e-4, 2 x the fp32 oracle's own
@@ -29,6 +29,7 @@ import torch
 
 from oracle import nerf_oracle as O
 import grad64
+from parity import assert_forward
 from screening import pdf_flips
 
 pytestmark = pytest.mark.gpu
@@ -121,18 +122,7 @@ def test_cfg4_rank_batch_matches_oracle():
                             rng=O.ReplayRNG(draws), capture=ocap)
     bad = _screen(cap, ocap, draws)
     assert bad.mean() <= 0.01, f"{bad.sum()} rays with a sample_pdf bin flip"
-    assert sorted(res) == sorted(ref)
-    for k in ref:
-        got, exp = res[k].cpu().numpy(), ref[k].numpy()
-        assert got.shape == exp.shape, k
-        err = np.abs(got - exp)
-        if k.startswith("depth"):
-            err = err / np.maximum(1.0, np.abs(exp))
-        err = err.reshape(err.shape[0], -1).max(1)
-        ok = (err <= 1e-4) | bad
-        assert ok.all(), f"{k}: max err {err[~bad].max():.3g} on {int((~ok).sum())} rays"
-    w = cap["weights_coarse"].cpu().numpy()
-    assert np.abs(w - ocap["weights_coarse"].numpy()).max() <= 1e-4
+    assert_forward(res, ref, cap, ocap, bad, label="cfg4 rank batch")
     print(f"cfg4 rank batch: {int(bad.sum())} of {B} rays screened (sample_pdf knot flips)")
 
 
@@ -156,7 +146,7 @@ def _oracle_point(dt, ulp, rays, draws, z_fine=None):
     cap = {}
     out = O.render_rays(ps, rays.to(dt), S, False, 1.0, 1.0, I, 32768, False,
                         rng=O.ReplayRNG([d.to(dt) for d in draws]), capture=cap,
-                        z_fine_override=z_fine)
+                        z_fine_override=z_fine, fp32_positions=dt == torch.float64)
     return ps, out, cap
 
 
@@ -175,12 +165,39 @@ def _kinks(models, rays, cap, c64, draws):
     return kc | kf
 
 
+def _mlp_kinks(saves, rays, cap, gmags):
+    """rays with an MLP ReLU our forward switched against float64, coarse or
+    fine (grad64.mlp_flips on the activations the training forward saved),
+    every one explained by a float64 pre-activation within 1e-5 of its kink"""
+    from oracle.nerf_oracle import embed
+    p64 = [{k: v.double() for k, v in p.items()} for p in _params()]
+    out = np.zeros(rays.shape[0], bool)
+    counts = []
+    for (save, n, _), z, p, gm in zip(saves, (cap["z_coarse"], cap["z_fine"]), p64, gmags):
+        z = z.detach().cpu()
+        spr = z.shape[1]
+        xyz = (rays[:, None, :3] + rays[:, None, 3:6] * z[:, :, None]).reshape(-1, 3)
+        x64 = torch.cat([embed(xyz.double(), 10),
+                         embed(rays[:, 3:6].double(), 4).repeat_interleave(spr, 0)], 1)
+        flip, expl, n_all = grad64.mlp_flips(save, n, x64, p, gmag=gm)
+        assert expl.all(), f"an MLP ReLU switched away from its kink: samples {np.nonzero(~expl)[0][:8]}"
+        counts.append((n_all, int(flip.sum())))
+        out |= flip.reshape(-1, spr).any(1)
+    print(f"cfg4: MLP ReLU flips against float64 (coarse, fine: all samples, samples with a "
+          f"gradient >= 1e-5 of the largest): {counts}")
+    return out
+
+
 @pytest.mark.parametrize("math_", ["f16x3", "fp32"])
 def test_cfg4_training_step_gradients_match_oracle(math_, monkeypatch):
     """every parameter gradient within max(1e-4, 2 x the fp32 oracle's own
-    distance from float64) of the float64 oracle (tests/grad64.py)"""
-    from nerf_pl_amd import ops
+    distance from float64) of the float64 oracle (tests/grad64.py), the float64
+    evaluations on the fp32 sample positions our kernels see (the oracle's
+    fp32_positions), so the floor measures the MLP's and the compositing's
+    accumulation, not the input rounding"""
+    from nerf_pl_amd import functions, ops
     monkeypatch.setattr(ops, "MATH", math_)
+    monkeypatch.setattr(functions, "_DEBUG", {})
     torch.set_num_threads(16)
     n = 1024
     _, _, _, rays, rgbs = _batch()
@@ -190,6 +207,8 @@ def test_cfg4_training_step_gradients_match_oracle(math_, monkeypatch):
     models = _models()
     cap = {}
     res = _ours(models, rays, draws, cap)
+    saves = functions._DEBUG["fwd_saves"]
+    assert len(saves) == 2 and saves[0][1] == n * S and saves[1][1] == n * (S + I)
     # the forward at the reference's own depths: every depth that moved is a
     # sample_pdf knot flip (asserted in _screen)
     (_, _, c32) = _oracle_point(torch.float32, None, rays, draws)
@@ -201,11 +220,16 @@ def test_cfg4_training_step_gradients_match_oracle(math_, monkeypatch):
     # depth bound above covers, not a gradient one
     zf = cap["z_fine"].detach().cpu()
     pts = {u: (_oracle_point(torch.float32, u, rays, draws, zf), _oracle_point(torch.float64, u, rays, draws, zf))
-           for u in (None, 1, 2)}
+           for u in grad64.FLOOR_POINTS}
     (_, _, c64) = pts[None][1]
     # rays whose compositing ReLU switched between ours and float64 leave the
     # loss (tests/grad64.py)
     bad = _kinks(models, rays, cap, c64, draws)
+    # ... and so are rays with an MLP ReLU our forward switched against float64
+    # on a sample whose output gradient matters (float64 d raw of the loss)
+    gm = torch.autograd.grad(_loss(pts[None][1][1], rgbs, torch.ones(n, dtype=torch.bool)),
+                             [c64["raw_coarse"], c64["raw_fine"]], retain_graph=True)
+    bad |= _mlp_kinks(saves, rays, cap, [g.abs().amax(1) for g in gm])
     assert bad.mean() <= 0.02, f"{bad.sum()} rays screened"
     keep = torch.from_numpy(~bad)
     _loss(res, rgbs, keep).backward()
@@ -217,9 +241,11 @@ def test_cfg4_training_step_gradients_match_oracle(math_, monkeypatch):
         _loss(o64, rgbs, keep).backward()
         g32s.append({f"m{i}.{k}": v.grad for i, p in enumerate(p32) for k, v in p.items()})
         g64s.append({f"m{i}.{k}": v.grad for i, p in enumerate(p64) for k, v in p.items()})
-    floor = grad64.fp32_floor(g32s, g64s)
+    spread = {}
+    floor = grad64.fp32_floor(g32s, g64s, spread)
     g64 = {f"m{i}.{k}": v.grad for i, p in enumerate(pts[None][1][0]) for k, v in p.items()}
     worst, where = grad64.check(ours, g64, floor, label=f"cfg4 {math_}")
     assert math.isfinite(worst)
     print(f"cfg4 {math_} gradients: worst {worst:.2f} of its bound ({where}, fp32 floor "
-          f"{floor[where]:.3g}, {len(g32s)} floor points)")
+          f"{floor[where]:.3g}, {len(g32s)} floor points: "
+          + " ".join(f"{v:.2g}" for v in spread[where]) + ")")

@@ -3,8 +3,9 @@
 * full BASELINE batches (cfg2: 4096 rays, 64+128, near/far 1/200; cfg3: 4096
   NDC rays, 64+64) against the CPU oracle (the reference's algorithm,
   tests/test_oracle_golden.py pins it to the reference) with the reference's
-  draws replayed: 1e-4 abs on rgb/opacity, 1e-4 relative on depth (north
-  star), sample_pdf bin flips screened per ray as in test_gpu_render.py;
+  draws replayed: 1e-4 ABSOLUTE on rgb, depth, opacity and the coarse and
+  fine weights (north star, tests/parity.py), sample_pdf bin flips screened
+  per ray as in test_gpu_render.py;
 * size-independent properties past what the oracle finishes in seconds:
   a ray's outputs do not depend on the rest of its batch (bit-exact, 65,536
   rays), and the parameter gradient of a summed loss is additive over a
@@ -19,6 +20,7 @@ import pytest
 import torch
 
 from oracle import nerf_oracle as O
+from parity import assert_forward
 from screening import pdf_flips
 
 pytestmark = pytest.mark.gpu
@@ -64,17 +66,18 @@ def _ours(models, rays, S, I, draws, perturb=1.0, noise=1.0, grad=False, cap=Non
                            rng=ReplayRNG(draws), _capture=cap)
 
 
-def _compare(res, ref, bad, tol=1e-4):
-    for k in ref:
-        got = res[k].detach().cpu().numpy()
-        exp = ref[k].numpy()
-        assert got.shape == exp.shape, k
-        err = np.abs(got - exp)
-        if k.startswith("depth"):
-            err = err / np.maximum(1.0, np.abs(exp))
-        err = err.reshape(err.shape[0], -1).max(1)
-        ok = (err <= tol) | bad
-        assert ok.all(), f"{k}: max err {err[~bad].max():.3g} on {int((~ok).sum())} rays"
+def _screen(cap, ocap, draws, limit=0.01):
+    """rays whose fine depths moved (a sample_pdf bin flip), every one
+    explained by a reference u within 1e-5 of a CDF knot (screening.pdf_flips)"""
+    if "z_fine" not in cap:
+        return np.zeros(cap["z_coarse"].shape[0], bool)
+    bad = (cap["z_fine"].cpu().numpy() != ocap["z_fine"].numpy()).any(1)
+    moved, explained = pdf_flips(cap["z_fine"], ocap, draws[-3])
+    assert not (bad & ~moved).any(), "z_fine differs although every importance depth matches"
+    assert not (moved & ~explained).any(), \
+        f"z_fine moved away from any CDF knot: rays {np.nonzero(moved & ~explained)[0][:8]}"
+    assert bad.mean() <= limit, f"{bad.sum()} rays with a sample_pdf bin flip"
+    return bad
 
 
 @pytest.mark.parametrize("kind", ["cfg2", "cfg3"])
@@ -96,20 +99,9 @@ def test_full_batch_matches_oracle(kind):
     ocap = {}
     ref = O.render_rays(params, rays, S, False, 1.0, 1.0, I, 32768, False,
                         rng=O.ReplayRNG(draws), capture=ocap)
-    zf = cap["z_fine"].cpu().numpy()
-    bad = np.abs(zf - ocap["z_fine"].numpy()).max(1) > 1e-4 * np.maximum(1, np.abs(zf).max(1))
-    # every screened ray explained: a reference importance depth missing from
-    # ours, its u within 1e-5 of a reference CDF knot (screening.pdf_flips)
-    moved, explained = pdf_flips(cap["z_fine"], ocap, draws[-3])
-    assert not (bad & ~moved).any(), "z_fine differs although every importance depth matches"
-    assert not (moved & ~explained).any(), \
-        f"z_fine moved away from any CDF knot: rays {np.nonzero(moved & ~explained)[0][:8]}"
-    assert bad.mean() <= 0.01, f"{bad.sum()} rays with a sample_pdf bin flip"
-    assert sorted(res) == sorted(ref)
-    _compare(res, ref, bad)
-    # the coarse weights that feed sample_pdf (the north star's "weights")
-    w = cap["weights_coarse"].detach().cpu().numpy()
-    assert np.abs(w - ocap["weights_coarse"].numpy()).max() <= 1e-4
+    bad = _screen(cap, ocap, draws)
+    # rgb / depth / opacity and the coarse and fine weights, 1e-4 absolute
+    assert_forward(res, ref, cap, ocap, bad, label=kind)
 
 
 def test_rays_do_not_depend_on_their_batch():
@@ -123,17 +115,15 @@ def test_rays_do_not_depend_on_their_batch():
     models = _models()
     full = _ours(models, rays, S, I, draws)
     idx = torch.arange(7, n, n // 512)[:512]
-    part = _ours(models, rays[idx].contiguous(), S, I, _slice_draws(draws, idx))
+    cap, ocap = {}, {}
+    part = _ours(models, rays[idx].contiguous(), S, I, _slice_draws(draws, idx), cap=cap)
     for k in part:
         assert torch.equal(full[k][idx.to(DEV)], part[k]), k
     params = [O.make_params(11, sigma_bias=0.5), O.make_params(12, sigma_bias=0.5)]
     ref = O.render_rays(params, rays[idx].contiguous(), S, False, 1.0, 1.0, I, 32768, False,
-                        rng=O.ReplayRNG(_slice_draws(draws, idx)))
-    zf_bad = np.zeros(512, bool)   # a bin flip shows up as a depth mismatch; allow a few
-    errs = np.abs(part["depth_fine"].cpu().numpy() - ref["depth_fine"].numpy())
-    zf_bad |= errs > 1e-4 * np.maximum(1, np.abs(ref["depth_fine"].numpy()))
-    assert zf_bad.mean() <= 0.01
-    _compare(part, ref, zf_bad)
+                        rng=O.ReplayRNG(_slice_draws(draws, idx)), capture=ocap)
+    bad = _screen(cap, ocap, _slice_draws(draws, idx))
+    assert_forward(part, ref, cap, ocap, bad, label="512 of 65536")
 
 
 @pytest.mark.parametrize("math", ["f16x3", "bf16"])
@@ -180,10 +170,11 @@ def test_single_ray_and_single_sample():
     rays = blender_rays(16, 1, near=2.0, far=6.0)[100:101].contiguous()
     for S, I in ((64, 128), (3, 1), (1, 0)):
         draws = _draws(1, S, I, 1.0, 2)
-        res = _ours(_models(), rays, S, I, draws)
+        cap, ocap = {}, {}
+        res = _ours(_models(), rays, S, I, draws, cap=cap)
         ref = O.render_rays(params, rays, S, False, 1.0, 1.0, I, 32768, False,
-                            rng=O.ReplayRNG(draws))
-        _compare(res, ref, np.zeros(1, bool))
+                            rng=O.ReplayRNG(draws), capture=ocap)
+        assert_forward(res, ref, cap, ocap, np.zeros(1, bool), label=f"1 ray S={S} I={I}")
 
 
 def test_empty_batch_raises_like_reference():

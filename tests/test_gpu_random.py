@@ -28,6 +28,7 @@ import torch
 
 from oracle import nerf_oracle as O
 import grad64
+from parity import assert_forward
 from screening import pdf_flips
 
 pytestmark = pytest.mark.gpu
@@ -101,6 +102,7 @@ def _run(c, grad=False, want_cap=False):
         moved, explained = pdf_flips(cap["z_fine"], ocap, draws[-3])
         assert not (bad & ~moved).any(), f"z_fine differs without a moved importance depth, {c}"
         assert not (moved & ~explained).any(), f"z_fine moved away from any CDF knot, {c}"
+    cap["_oracle"] = {k: v.detach() for k, v in ocap.items()}
     return (models, params, res, ref, bad, cap) if want_cap else (models, params, res, ref, bad)
 
 
@@ -114,18 +116,10 @@ def test_random_config_matches_oracle(seed, math, monkeypatch):
     from nerf_pl_amd import ops
     monkeypatch.setattr(ops, "MATH", math)
     c = _config(seed)
-    _, _, res, ref, bad = _run(c)
+    _, _, res, ref, bad, cap = _run(c, want_cap=True)
     assert bad.sum() <= max(1, 0.02 * c["n"]), f"{bad.sum()} sample_pdf bin flips in {c}"
-    assert sorted(res) == sorted(ref), c
-    for k in ref:
-        got, exp = res[k].detach().cpu().numpy(), ref[k].detach().numpy()
-        assert got.shape == exp.shape, (k, c)
-        err = np.abs(got - exp)
-        if k.startswith("depth"):
-            err = err / np.maximum(1.0, np.abs(exp))
-        err = err.reshape(err.shape[0], -1).max(1)
-        ok = (err <= 1e-4) | bad
-        assert ok.all(), f"{k}: max err {err[~bad].max():.3g} on {int((~ok).sum())} rays, {c}"
+    # rgb / depth / opacity and both passes' weights, 1e-4 absolute (tests/parity.py)
+    assert_forward(res, ref, cap, cap["_oracle"], bad, label=f"{math} {c}")
 
 
 def _oracle_grads(c, rays, draws, dt, ulp=None, z_fine=None):
@@ -139,7 +133,8 @@ def _oracle_grads(c, rays, draws, dt, ulp=None, z_fine=None):
     cap = {}
     args = (c["S"], c["use_disp"], c["perturb"], c["noise"], c["I"], 32768, c["white_back"], False)
     ref = O.render_rays(params, rays.to(dt), *args, rng=O.ReplayRNG([d.to(dt) for d in draws]),
-                        capture=cap, z_fine_override=z_fine)
+                        capture=cap, z_fine_override=z_fine,
+                        fp32_positions=dt == torch.float64)
     return params, ref, cap
 
 
@@ -170,6 +165,26 @@ def _kinks(c, models, rays, draws, cap, cap64):
     return out
 
 
+def _mlp_kinks(c, saves, rays, cap, params, gmags):
+    """rays with an MLP ReLU our training forward switched against float64
+    (tests/grad64.py mlp_flips), every one explained by a float64
+    pre-activation within 1e-5 of its kink"""
+    passes = [cap["z_coarse"]] + ([cap["z_fine"]] if c["I"] > 0 else [])
+    assert len(saves) == len(passes)
+    out = np.zeros(c["n"], bool)
+    for (save, n, _), z, p, gm in zip(saves, passes, params, gmags):
+        z = z.detach().cpu()
+        spr = z.shape[1]
+        xyz = (rays[:, None, :3] + rays[:, None, 3:6] * z[:, :, None]).reshape(-1, 3)
+        x64 = torch.cat([O.embed(xyz.double(), 10),
+                         O.embed(rays[:, 3:6].double(), 4).repeat_interleave(spr, 0)], 1)
+        flip, expl, _ = grad64.mlp_flips(save, n, x64, {k: v.detach().double() for k, v in p.items()},
+                                         gmag=gm)
+        assert expl.all(), f"an MLP ReLU switched away from its kink, {c}"
+        out |= flip.reshape(-1, spr).any(1)
+    return out
+
+
 def _named(models_or_params, zeros_like=None):
     out = {}
     for i, m in enumerate(models_or_params):
@@ -186,23 +201,37 @@ def _named(models_or_params, zeros_like=None):
 def test_random_config_gradients_match_oracle(seed, math, monkeypatch):
     """every parameter gradient within max(1e-4, 2 x the fp32 oracle's own
     distance from float64) of the float64 oracle (tests/grad64.py)"""
-    from nerf_pl_amd import ops
+    from nerf_pl_amd import functions, ops
     monkeypatch.setattr(ops, "MATH", math)
+    monkeypatch.setattr(functions, "_DEBUG", {})
     c = _config(seed)
     c["test_time"] = False
     c["n"] = max(c["n"], 64)
-    models, _, res, _, _, cap_ours = _run(c, grad=True, want_cap=True)   # asserts the forward
+    models, params, res, _, _, cap_ours = _run(c, grad=True, want_cap=True)   # asserts the forward
+    saves = functions._DEBUG["fwd_saves"]
     rays, draws = _rays(c), _draws(c)
     # every evaluation's fine pass at our depths (the reference detaches them,
     # rendering.py:253-255; see test_gpu_cfg4.py)
     zf = cap_ours["z_fine"].detach().cpu() if c["I"] > 0 else None
     pts = {u: (_oracle_grads(c, rays, draws, torch.float32, u, zf),
-               _oracle_grads(c, rays, draws, torch.float64, u, zf)) for u in (None, 1, 2)}
+               _oracle_grads(c, rays, draws, torch.float64, u, zf)) for u in grad64.FLOOR_POINTS}
     (_, _, cap64) = pts[None][1]
     # rays whose compositing ReLU switched between ours and float64 are screened
     bad = _kinks(c, models, rays, draws, cap_ours, cap64)
+    # ... and rays with an MLP ReLU our forward switched against float64 on a
+    # sample whose output gradient matters (float64 d raw of the functional)
+    raws = [cap64["raw_coarse"]] + ([cap64["raw_fine"]] if c["I"] > 0 else [])
+    gm = torch.autograd.grad(_functional(pts[None][1][1], torch.ones(c["n"], dtype=torch.bool), seed),
+                             raws, retain_graph=True)
+    mk = _mlp_kinks(c, saves, rays, cap_ours, params, [g.abs().amax(1) for g in gm])
+    print(f"{seed} {math}: {int(bad.sum())} rays with a compositing ReLU kink, {int(mk.sum())} with "
+          f"an MLP ReLU flip, {int((bad | mk).sum())} of {c['n']} screened")
+    bad |= mk
     keep = torch.from_numpy(~bad)
-    assert bad.sum() <= max(1, 0.05 * c["n"]), f"{bad.sum()} rays screened, {c}"
+    # at most 10% of the rays: with up to 237 samples per ray x 2,304 ReLUs per
+    # sample, an fp32 forward (ours or any) switches a few kinks on samples
+    # that carry gradient (case 105: 10-17 of 281 rays, in both arithmetics)
+    assert bad.sum() <= max(1, 0.1 * c["n"]), f"{bad.sum()} rays screened, {c}"
     _functional(res, keep, seed).backward()
     g32s, g64s = [], []
     for u, ((p32, r32, k32), (p64, r64, k64)) in pts.items():
