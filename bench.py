@@ -66,8 +66,16 @@ HBM_PEAK_GBS = 8000.0
 FLOP_FWD = 1_186_816
 FLOP_FWD_SIGMA = 982_528
 FLOP_DGRAD = 1_115_392
-FLOP_WGRAD = 1_186_816
-FLOP_TRAIN = FLOP_FWD + FLOP_DGRAD + FLOP_WGRAD   # 3,489,024
+# the reference algorithm's weight-gradient FLOPs per sample (autograd's
+# sum dz x^T of every layer) ...
+FLOP_WGRAD_REF = 1_186_816
+# ... and what the kernels execute: xyz_encoding_final's per-sample term
+# (2 * 256 * 256, its input feat is not saved) is replaced by the per-launch
+# products of nr_wgrad_dir_feat (G W_final^T and W_dir^T G, 2 x 2*128*256*256,
+# plus W_dir^T db: DIRFEAT_FLOP), whose launches the rooflines time with it
+FLOP_WGRAD = FLOP_WGRAD_REF - 2 * 256 * 256                     # 1,055,744
+DIRFEAT_FLOP = 2 * (2 * 128 * 256 * 256) + 2 * 256 * 128       # 33,619,968 per launch
+FLOP_TRAIN = FLOP_FWD + FLOP_DGRAD + FLOP_WGRAD_REF   # 3,489,024 (reference algorithm)
 # sigma-only graph trained (cfg5): forward + weight-grad of the sigma-only
 # layers, data-grad without the two PE inputs (layer 1 and layer 5's skip)
 FLOP_TRAIN_SIGMA = 2 * FLOP_FWD_SIGMA + 2 * (FLOP_FWD_SIGMA // 2 - 2 * 63 * 256)
@@ -97,21 +105,23 @@ KERNEL_FLOP = {"mlp_fwd": FLOP_FWD, "mlp_fwd_sigma": FLOP_FWD_SIGMA,
 CONFIGS = ("cfg2", "cfg3", "cfg4", "cfg5", "eval")
 
 
-def kernel_roofline(k, events, math_, traffic_json):
+def kernel_roofline(k, events, math_, traffic_json, extra=None):
     """Roofline of one MLP kernel from its largest (fine-pass) launches, timed
     with HIP events on the stream it runs on.  The weight gradient streams every
     saved segment once at 60 FLOP/B: HBM-bound (algorithmic bytes); the fused
     forward and data-gradient chains are MFMA-bound (algorithmic FLOPs of the
-    fp32 products)."""
+    fp32 products).  ``extra`` = (ms, FLOP) of a follow-up launch that belongs
+    to each launch of this kernel (the weight gradient's nr_wgrad_dir_feat):
+    its time and work are added to the launch's."""
     big = [(ev[0].elapsed_time(ev[1]), ev[2], active_samples(ev)) for ev in events]
     nmax = max(n for _, n, _ in big)
     durs = [t for t, n, _ in big if n == nmax]
-    avg = sum(durs) / len(durs)
+    avg = sum(durs) / len(durs) + (extra[0] if extra else 0.0)
     # samples the fine-pass launches actually worked on (the backward skips
     # the blocks whose output gradient is exactly zero)
     nwork = sum(w for _, n, w in big if n == nmax) / len(durs)
     flops = KERNEL_FLOP[k]
-    tflops = flops * nwork / (avg * 1e-3) / 1e12
+    tflops = (flops * nwork + (extra[1] if extra else 0)) / (avg * 1e-3) / 1e12
     traffic, tsrc = None, None
     t = traffic_json.get(f"{math_}/{k}") or traffic_json.get(k)
     if t and int(t["samples"]) == nmax and t.get("arithmetic", math_) == math_:
@@ -843,9 +853,16 @@ def main():
                     tj = {k: dict(v, file=rel) for k, v in json.load(open(tf)).items()
                           if isinstance(v, dict)}
                     break
+            # nr_wgrad_dir_feat finishes every full-graph weight gradient (one
+            # launch each): its average launch is part of mlp_wgrad's
+            df = ks.get("wgrad_dir_feat")
             for k in KERNEL_FLOP:
                 if k in ks:
-                    roofs[k] = kernel_roofline(k, timer.events[k], math_, tj)
+                    roofs[k] = kernel_roofline(k, timer.events[k], math_, tj,
+                                               extra=(df["avg_ms"], DIRFEAT_FLOP)
+                                               if k == "mlp_wgrad" and df else None)
+                    if k == "mlp_wgrad" and df:
+                        roofs[k]["includes"] = "nr_wgrad_dir_feat (one launch per weight gradient)"
             if roofs:
                 dom = max(roofs, key=lambda k: ks[k]["total_ms"])
                 roof = roofs[dom]
@@ -854,8 +871,12 @@ def main():
                 # gradients) against the fp32 MFMA peak -- the north star's ratio
                 fl = sum(KERNEL_FLOP[k] * active_samples(ev) for k in roofs for ev in timer.events[k])
                 t = sum(ks[k]["total_ms"] for k in roofs)
+                if df and "mlp_wgrad" in roofs:
+                    fl += DIRFEAT_FLOP * df["launches"]
+                    t += df["total_ms"]
                 tf_ = fl / (t * 1e-3) / 1e12
-                stage = dict(kernels=sorted(roofs), ms_per_step=round(t / steps, 4),
+                stage = dict(kernels=sorted(roofs) + (["wgrad_dir_feat"] if df else []),
+                             flop_per_step=int(fl / steps), ms_per_step=round(t / steps, 4),
                              share_of_step=round(t / (ms * steps), 4),
                              tflops_fp32_equiv=round(tf_, 2),
                              fp32_mfma_peak=FP32_MFMA_PEAK_TF,
@@ -952,7 +973,18 @@ def main():
                        "global_batch": wl["rays_per_step"] * world,
                        "samples_per_ray": wl["samples_per_ray"],
                        "parallelism": f"dp{world}" if wl["train"] else f"replicas{world}"},
-            "model_tflops": round(rays_per_s * wl["flop_per_ray"] / 1e12, 2),
+            # the MLP work the kernels executed (every launch, the samples the
+            # backward listed) per second of the whole step -- mlp_stage's FLOPs
+            # over the step time -- and the reference algorithm's nominal count
+            # (every sample through forward and both gradients), which the
+            # zero-gradient skip never does
+            "model_tflops": (round(stage["flop_per_step"] / (ms * 1e-3) / 1e12, 2)
+                             if stage else None),
+            "model_tflops_nominal": round(rays_per_s * wl["flop_per_ray"] / 1e12, 2),
+            "model_tflops_basis": ("model_tflops: mlp_stage.flop_per_step (the MLP FLOPs executed, "
+                                   "fp32-equivalent) / ms_per_step; model_tflops_nominal: the "
+                                   "reference algorithm's FLOPs per ray (forward + data + weight "
+                                   "gradient of every sample) x rays/s"),
             "roofline": roof,
             "rooflines": roofs,
             "mlp_stage": stage,

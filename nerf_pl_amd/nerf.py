@@ -17,6 +17,8 @@ parameter names (models/nerf.py:4-124), backed by the fused HIP kernels.
   device: the reference's layer sequence on PyTorch-ROCm GEMMs, with
   ``render_rays``'s sampling and compositing still on the HIP kernels
   (SURVEY.md 8b).  Every caller of the reference uses the defaults.
+* Host (CPU) inputs run the same layer sequence on the host
+  (nerf_pl_amd.host, BASELINE configs[0]).
 """
 from __future__ import annotations
 
@@ -45,9 +47,7 @@ class Embedding(nn.Module):
         self._fused = in_channels == 3 and logscale and N_freqs < 31
 
     def forward(self, x):
-        if not x.is_cuda:
-            raise ValueError("nerf_pl_amd.Embedding: input must be a HIP device tensor")
-        if self._fused:
+        if self._fused and x.is_cuda:
             shp = x.shape
             out = ops.embed(x.reshape(-1, 3), self.N_freqs)
             return out.view(*shp[:-1], self.out_channels)
@@ -132,16 +132,19 @@ class NeRF(nn.Module):
         return c[1], c[2]
 
     def forward(self, x, sigma_only=False):
-        if not self._fused:
+        if not self._fused or not x.is_cuda:
+            # a host input (nerf_pl_amd.host) or a configuration the fused
+            # kernels do not implement: the layer sequence
             return self.forward_layers(x, sigma_only)
         from .functions import mlp_apply
         return mlp_apply(self, x=x, sigma_only=sigma_only)
 
     def forward_layers(self, x, sigma_only=False):
-        """nerf.py:83-124 as a sequence of device GEMMs (configurations the fused
-        kernels do not implement)."""
-        if not x.is_cuda:
-            raise ValueError("nerf_pl_amd.NeRF: input must be a HIP device tensor")
+        """nerf.py:83-124 as a sequence of GEMMs on the parameters' device
+        (configurations the fused kernels do not implement; host batches)."""
+        dev = self.sigma.weight.device
+        if x.device != dev:
+            raise ValueError(f"nerf_pl_amd.NeRF: input on {x.device}, parameters on {dev}")
         if not sigma_only:
             input_xyz, input_dir = torch.split(x, [self.in_channels_xyz, self.in_channels_dir], -1)
         else:

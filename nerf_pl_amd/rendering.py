@@ -14,18 +14,38 @@ Drop-in notes
   embeddings or NeRF configuration takes the composable path (the reference's
   ``inference`` sequence -- xyz, embeddings, model -- on device GEMMs), with
   sampling and compositing on the same HIP kernels either way.
-* Everything runs on the HIP device that holds ``rays``; there is no CPU path.
+* Everything runs on the HIP device that holds ``rays``.  A batch on the host
+  (BASELINE configs[0], "PyTorch CPU, plumbing") runs nerf_pl_amd.host: the
+  reference's sequence in PyTorch CPU ops, as the reference itself runs on
+  whichever device ``rays`` lives (rendering.py:178, 216, 231).  The choice is
+  the batch's device alone: a HIP-device batch runs the kernels or raises.
 """
 from __future__ import annotations
+
+import functools
+import os
 
 import torch
 
 from . import ops
 from .functions import composite_apply, mlp_apply
 from .rng import (STREAM_JITTER, STREAM_NOISE_COARSE, STREAM_NOISE_FINE, STREAM_PERTURB,
-                  STREAM_U, PhiloxRNG)
+                  STREAM_U, PhiloxRNG, TorchRNG)
 
 __all__ = ["render_rays", "sample_pdf"]
+
+# A training call runs the fine pass (MLP forward + compositing) on a side
+# stream, so that autograd -- which runs every backward node on the stream its
+# forward ran on -- executes the fine model's backward there too, beside the
+# coarse model's on the caller's stream: the two chains are independent after
+# sample_pdf's detach (rendering.py:253-255) and fill each other's kernel
+# tails.  NERF_PL_AMD_FINE_STREAM=0 keeps everything on the caller's stream.
+FINE_STREAM = os.environ.get("NERF_PL_AMD_FINE_STREAM", "1") != "0"
+
+
+@functools.lru_cache(maxsize=None)
+def _side_stream(device_index: int):
+    return torch.cuda.Stream(device=torch.device("cuda", device_index))
 
 
 def _fused_ok(models, embeddings):
@@ -87,6 +107,15 @@ def sample_pdf(rays, weights, N_importance, det=False, eps=1e-5, *, rng=None):
 def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=0, noise_std=1,
                 N_importance=0, chunk=1024 * 32, white_back=False, test_time=False, *, rng=None,
                 _capture=None):
+    if isinstance(rays, torch.Tensor) and rays.device.type == "cpu":
+        if rays.dtype != torch.float32:
+            raise TypeError(f"rays: expected float32, got {rays.dtype}")
+        if rays.dim() != 2 or rays.shape[-1] != 8:
+            raise ValueError(f"rays: expected (N, 8), got {tuple(rays.shape)}")
+        from .host import render_rays_host
+        return render_rays_host(models, embeddings, rays, N_samples, use_disp, perturb, noise_std,
+                                N_importance, chunk, white_back, test_time,
+                                TorchRNG() if rng is None else rng, _capture)
     del chunk
     fused = _fused_ok(models, embeddings)
 
@@ -139,10 +168,29 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
                                 z_coarse=z_c, merge=True)
         cap["z_fine"] = z_f
         s_f = N_samples + N_importance
-        noise_f = rng.randn((n_rays, s_f), dev)
-        raw_f = mlp(models[1], z_f, s_f)
-        rgb_f, depth_f, opac_f, w_f = composite_apply(raw_f, z_f, rays, noise_f, noise_std, seed,
-                                                      STREAM_NOISE_FINE, white_back)
+
+        def fine_pass():
+            noise_f = rng.randn((n_rays, s_f), dev)
+            raw_f = mlp(models[1], z_f, s_f)
+            return composite_apply(raw_f, z_f, rays, noise_f, noise_std, seed, STREAM_NOISE_FINE,
+                                   white_back)
+
+        if FINE_STREAM and torch.is_grad_enabled() and any(
+                p.requires_grad for p in models[1].parameters()):
+            main = torch.cuda.current_stream(dev)
+            side = _side_stream(dev.index)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                outs = fine_pass()
+            main.wait_stream(side)
+            # the caching allocator must not hand out blocks one stream still uses
+            for t in (rays, z_f):
+                t.record_stream(side)
+            for t in outs:
+                t.record_stream(main)
+            rgb_f, depth_f, opac_f, w_f = outs
+        else:
+            rgb_f, depth_f, opac_f, w_f = fine_pass()
         cap["weights_fine"] = w_f
         result["rgb_fine"] = rgb_f
         result["depth_fine"] = depth_f

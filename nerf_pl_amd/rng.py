@@ -10,6 +10,10 @@ The reference draws five tensors from the global torch generator per call
   Distribution-equivalent to the reference, not stream-identical.
 * :class:`ReplayRNG`: replays recorded tensors in draw order -- used for
   bit-level parity with the reference (tests/golden).
+* :class:`TorchRNG`: draws from the global torch generator exactly as the
+  reference does (``torch.rand`` / ``torch.randn`` on the rays' device) -- the
+  default of a host batch (nerf_pl_amd.host), which then consumes the same
+  numbers as the reference under the same ``torch.manual_seed``.
 """
 from __future__ import annotations
 
@@ -50,3 +54,13 @@ class ReplayRNG:
 
     def exhausted(self) -> bool:
         return self._pos == len(self._queue)
+
+
+class TorchRNG:
+    seed = 0
+
+    def rand(self, shape, device):
+        return torch.rand(*shape, device=device)
+
+    def randn(self, shape, device):
+        return torch.randn(*shape, device=device)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # The one driver of GPU-box work (replaces the per-round drivers of rounds 3-4):
 #
-#   bash scripts/gpu.sh <tag> <step> [<step> ...]          outputs: gpurun_out/$R/<tag>/ (R: round, default r05)
+#   bash scripts/gpu.sh <tag> <step> [<step> ...]          outputs: gpurun_out/$R/<tag>/ (R: round, default r06)
 #
 # Steps run in order, each under its own time limit; the first failing step
 # ends the call (no GPU work after a fault, an abort or a time limit).
@@ -26,7 +26,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-R=${R:-r05}
+R=${R:-r06}
 tag=$1; shift
 out=gpurun_out/$R/$tag
 mkdir -p "$out"

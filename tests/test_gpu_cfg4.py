@@ -244,6 +244,10 @@ def test_cfg4_training_step_gradients_match_oracle(math_, monkeypatch):
     spread = {}
     floor = grad64.fp32_floor(g32s, g64s, spread)
     g64 = {f"m{i}.{k}": v.grad for i, p in enumerate(pts[None][1][0]) for k, v in p.items()}
+    fl = sorted(floor.values())
+    print(f"cfg4 {math_}: fp32 floors over {len(fl)} tensors: median {fl[len(fl) // 2]:.2g}, "
+          f"{sum(f <= 1e-4 for f in fl)} at or below 1e-4, largest {fl[-1]:.2g} "
+          f"({max(floor, key=floor.get)})")
     worst, where = grad64.check(ours, g64, floor, label=f"cfg4 {math_}")
     assert math.isfinite(worst)
     print(f"cfg4 {math_} gradients: worst {worst:.2f} of its bound ({where}, fp32 floor "

@@ -287,3 +287,46 @@ def test_inplace_parameter_change_before_backward_raises(defer, monkeypatch):
     out = mlp_apply(net, rays=rays, z=z, spr=32)
     out.sum().backward()
     assert torch.isfinite(net.xyz_encoding_final.weight.grad).all()
+
+
+def test_fine_stream_step_is_bitwise_the_single_stream_step(monkeypatch):
+    """A training call runs the fine pass (and so, by autograd's stream rule,
+    its backward) on a side stream beside the coarse pass's backward
+    (rendering.FINE_STREAM).  Same inputs, same draws: outputs and every
+    parameter gradient equal the single-stream step bit for bit, over three
+    steps with FusedAdam in between (the caching allocator's cross-stream
+    reuse is exercised by the repeated steps)."""
+    from nerf_pl_amd import Embedding, NeRF, ReplayRNG, rendering, render_rays
+    from nerf_pl_amd.optim import FusedAdam
+    from nerf_pl_amd.rays import blender_rays
+    rays = blender_rays(64, 1, near=1.0, far=200.0)[:1024].contiguous().to(DEV)
+    target = torch.rand(1024, 3, generator=torch.Generator().manual_seed(1)).to(DEV)
+    g = torch.Generator().manual_seed(2)
+    draws = [[torch.rand(1024, 64, generator=g), torch.randn(1024, 64, generator=g),
+              torch.rand(1024, 128, generator=g), torch.rand(1024, 128, generator=g),
+              torch.randn(1024, 192, generator=g)] for _ in range(3)]
+    runs = []
+    for fs in (False, True):
+        monkeypatch.setattr(rendering, "FINE_STREAM", fs)
+        models = []
+        for s in (41, 42):
+            m = NeRF()
+            m.load_state_dict(O.make_params(s, sigma_bias=0.5))
+            models.append(m.to(DEV))
+        opt = FusedAdam([p for m in models for p in m.parameters()], lr=5e-4)
+        outs = []
+        for d in draws:
+            res = render_rays(models, [Embedding(3, 10), Embedding(3, 4)], rays, 64, False, 1.0, 1.0,
+                              128, 32768, False, rng=ReplayRNG(d))
+            loss = ((res["rgb_coarse"] - target) ** 2).mean() + ((res["rgb_fine"] - target) ** 2).mean()
+            opt.zero_grad()
+            loss.backward()
+            outs.append({k: v.detach().clone() for k, v in res.items()})
+            outs.append({f"{i}.{k}": p.grad.clone() for i, m in enumerate(models)
+                         for k, p in m.named_parameters()})
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append(outs)
+    for a, b in zip(*runs):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
