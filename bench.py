@@ -126,7 +126,7 @@ def kernel_roofline(k, events, math_, traffic_json, extra=None):
     t = traffic_json.get(f"{math_}/{k}") or traffic_json.get(k)
     if t and int(t["samples"]) == nmax and t.get("arithmetic", math_) == math_:
         traffic = round(t["hbm_bytes"] / 1e9, 3)
-        tsrc = f"{t.get('file', 'profiles/r01/traffic.json')} ({t['method']})"
+        tsrc = f"{t.get('file', '?')} ({t['method']})"
     common = dict(kernel=k, traffic=traffic, traffic_unit="GB per launch", traffic_source=tsrc,
                   samples_per_launch=nmax, avg_launch_ms=round(avg, 4))
     if nwork != nmax:
@@ -823,6 +823,11 @@ def main():
         timer.events = {}
         if F_ is not None:
             F_.ACTIVE_LOG = []
+        # the timed region's time origin on the device: every kernel event's
+        # offset from it places launches of both streams on one clock (the
+        # MLP stage's busy time is the union of its launches' intervals)
+        timer.ref = torch.cuda.Event(enable_timing=True)
+        timer.ref.record()
         timer.enabled = True
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -845,9 +850,8 @@ def main():
         roof, roofs, stage = None, {}, None
         if ks:
             tj = {}
-            for rel in ("profiles/r05/late/traffic.json", "profiles/r05/traffic.json", "profiles/r04/traffic.json", "profiles/r03/traffic.json",
-                        "profiles/r02/traffic.json",
-                        "profiles/r01/traffic.json"):
+            for rel in ("profiles/r06/traffic.json", "profiles/r05/late/traffic.json",
+                        "profiles/r05/traffic.json"):
                 tf = os.path.join(REPO, rel)
                 if os.path.exists(tf):
                     tj = {k: dict(v, file=rel) for k, v in json.load(open(tf)).items()
@@ -874,9 +878,30 @@ def main():
                 if df and "mlp_wgrad" in roofs:
                     fl += DIRFEAT_FLOP * df["launches"]
                     t += df["total_ms"]
+                # the fine pass's backward runs on its own stream beside the
+                # coarse pass's (rendering.FINE_STREAM): the stage's time is the
+                # union of its launches' intervals on the device clock, not the
+                # sum of their (overlapping) durations
+                iv = sorted((timer.ref.elapsed_time(ev[0]), timer.ref.elapsed_time(ev[1]))
+                            for k in list(roofs) + (["wgrad_dir_feat"] if df else [])
+                            for ev in timer.events[k])
+                busy, cur = 0.0, None
+                for a0, a1 in iv:
+                    if cur is None or a0 > cur[1]:
+                        if cur is not None:
+                            busy += cur[1] - cur[0]
+                        cur = [a0, a1]
+                    else:
+                        cur[1] = max(cur[1], a1)
+                if cur is not None:
+                    busy += cur[1] - cur[0]
+                t_sum, t = t, busy
                 tf_ = fl / (t * 1e-3) / 1e12
                 stage = dict(kernels=sorted(roofs) + (["wgrad_dir_feat"] if df else []),
                              flop_per_step=int(fl / steps), ms_per_step=round(t / steps, 4),
+                             launch_ms_sum_per_step=round(t_sum / steps, 4),
+                             time_basis="union of the launches' intervals (HIP events, one clock; "
+                                        "the two passes' backward launches overlap)",
                              share_of_step=round(t / (ms * steps), 4),
                              tflops_fp32_equiv=round(tf_, 2),
                              fp32_mfma_peak=FP32_MFMA_PEAK_TF,
@@ -905,6 +930,20 @@ def main():
                 by_n.setdefault(ev[2], []).append(active_samples(ev) / ev[2])
             backward_blocks[k] = {f"samples_{n}": round(sum(v) / len(v), 4)
                                   for n, v in sorted(by_n.items())}
+    # per-kernel rooflines with the two passes serialised: in the timed region
+    # the fine pass's backward launches share the GPU with the coarse pass's
+    # (rendering.FINE_STREAM), so their HIP-event durations there are wall
+    # times under contention ("rooflines_concurrent"); a short pass on one
+    # stream gives each kernel's own launch time ("rooflines")
+    roofs_conc, roofs_iso = roofs, None
+    from nerf_pl_amd import rendering as _rendering
+    if wl["train"] and ks and _rendering.FINE_STREAM:
+        _rendering.FINE_STREAM = False
+        try:
+            el_i, _ = run(10, 3, "serialised kernels")
+        finally:
+            _rendering.FINE_STREAM = True
+        _, _, roofs_iso, _ = rooflines(math_main, el_i / 10 * 1e3, 10)
     # exact-fp32 leg: the same workload on v_mfma_f32_32x32x2_f32 (fp32
     # products, no operand splitting) -- its own roofline against the fp32
     # MFMA peak, next to the default arithmetic's
@@ -986,7 +1025,13 @@ def main():
                                    "reference algorithm's FLOPs per ray (forward + data + weight "
                                    "gradient of every sample) x rays/s"),
             "roofline": roof,
-            "rooflines": roofs,
+            "rooflines": roofs_iso or roofs,
+            "rooflines_basis": ("per-kernel launch times from 10 extra steps with both passes on "
+                                "one stream (the timed region overlaps the two backward chains); "
+                                "'roofline' (the dominant kernel, the forward, which never "
+                                "overlaps) comes from the timed region itself"
+                                if roofs_iso else "the timed region"),
+            "rooflines_concurrent": roofs_conc if roofs_iso else None,
             "mlp_stage": stage,
             "fp32_leg": fp32_leg,
             "backward_samples": backward_blocks,

@@ -72,7 +72,9 @@ __global__ void __launch_bounds__(kScanT) active_scan_kernel(int32_t* __restrict
         for (; b + 8 <= r1; b += 8)
 #pragma unroll
             for (int i = 0; i < 8; ++i) part[i] += cnt[b + i];
-        for (int i = 0; b < r1; ++b, ++i) part[i] += cnt[b];
+        // the tail (< 8 entries) goes to part[0]: a runtime index into part
+        // would put the array in scratch
+        for (; b < r1; ++b) part[0] += cnt[b];
 #pragma unroll
         for (int i = 0; i < 8; ++i) run += part[i];
     }

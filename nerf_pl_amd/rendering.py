@@ -41,11 +41,16 @@ __all__ = ["render_rays", "sample_pdf"]
 # sample_pdf's detach (rendering.py:253-255) and fill each other's kernel
 # tails.  NERF_PL_AMD_FINE_STREAM=0 keeps everything on the caller's stream.
 FINE_STREAM = os.environ.get("NERF_PL_AMD_FINE_STREAM", "1") != "0"
+# HIP priority of that stream (-1 high, 0 normal): the fine chain is the longer
+# one, so its workgroups are dispatched first and the coarse chain's fill the
+# CUs its kernel tails leave idle
+FINE_STREAM_PRIORITY = int(os.environ.get("NERF_PL_AMD_FINE_STREAM_PRIORITY", "0"))
 
 
 @functools.lru_cache(maxsize=None)
 def _side_stream(device_index: int):
-    return torch.cuda.Stream(device=torch.device("cuda", device_index))
+    return torch.cuda.Stream(device=torch.device("cuda", device_index),
+                             priority=FINE_STREAM_PRIORITY)
 
 
 def _fused_ok(models, embeddings):
