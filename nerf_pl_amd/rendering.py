@@ -41,9 +41,10 @@ __all__ = ["render_rays", "sample_pdf"]
 # sample_pdf's detach (rendering.py:253-255) and fill each other's kernel
 # tails.  NERF_PL_AMD_FINE_STREAM=0 keeps everything on the caller's stream.
 FINE_STREAM = os.environ.get("NERF_PL_AMD_FINE_STREAM", "1") != "0"
-# HIP priority of that stream (-1 high, 0 normal): the fine chain is the longer
-# one, so its workgroups are dispatched first and the coarse chain's fill the
-# CUs its kernel tails leave idle
+# HIP priority of that stream (-1 high, 0 normal).  Same-box A/B
+# (profiles/r06/ab_stream): side stream 510.4k vs one stream 497.0k rays/s;
+# priority -1 511.0k (no difference); the coarse pass on the side stream
+# instead (its backward then queues behind the fine one's) 507.1k vs 507.9k
 FINE_STREAM_PRIORITY = int(os.environ.get("NERF_PL_AMD_FINE_STREAM_PRIORITY", "0"))
 
 
