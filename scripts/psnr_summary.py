@@ -18,10 +18,13 @@ render draws, so their PSNRs are correlated (r ~ 0.5-0.7) and the per-seed
 difference has a smaller spread than two independent samples; mean and
 Student-t interval of the per-seed differences over the seeds both groups ran.
 Writes profiles/r05/psnr/summary.json (round 3's runs under profiles/r03/psnr,
-round 4's under profiles/r04/psnr and round 5's under profiles/r05/psnr, one group per seed).
+round 4's under profiles/r04/psnr and round 5's under profiles/r05/psnr, one group per seed;
+since round 6 each directory's run JSONs are packed into its runs.jsonl, read
+through the same file patterns).
 
     python scripts/psnr_summary.py
 """
+import fnmatch
 import glob
 import json
 import math
@@ -32,11 +35,24 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEPS = (500, 1000, 1500, 2000)
 
 
+def _files(pat):
+    """(basename, run) for every run matching pat: the JSON files themselves,
+    or the entries of their directory's runs.jsonl (round 6 packed each psnr
+    directory's runs into one file: {"file": basename, "run": the JSON})"""
+    for f in sorted(glob.glob(os.path.join(REPO, pat))):
+        yield os.path.basename(f), json.load(open(f))
+    d, base = os.path.split(pat)
+    for j in sorted(glob.glob(os.path.join(REPO, d, "runs.jsonl"))):
+        for line in open(j):
+            e = json.loads(line)
+            if fnmatch.fnmatch(e["file"], base):
+                yield e["file"], e["run"]
+
+
 def load(*patterns):
     runs = {}
     for pat in patterns:
-        for f in sorted(glob.glob(os.path.join(REPO, pat))):
-            d = json.load(open(f))
+        for f, d in _files(pat):
             if d.get("perturb_ulp") or "eval_weights" in d or "psnr" not in d:
                 continue
             seed = int(re.search(r"_s(\d+)", os.path.basename(f)).group(1))
