@@ -16,6 +16,21 @@
 // groups ahead; one barrier per group hands a slot over.  The B split of the
 // next k-step and the previous layer's saved-activation stores are spread
 // between the MFMAs of the current k-step.
+//
+// NR_FWD_W2 = 1 (f16x3): two waves per SIMD -- eight waves per workgroup,
+// each carrying one 16-sample tile of a 32-sample block (waves 2b, 2b+1 hold
+// block b's tiles S = 0, 1), as mlp_bwd3.hip's NR_BWD_W2.  Saved layouts are
+// unchanged; a block's ReLU mask words, which interleave both tiles' bits,
+// are combined from its two waves through LDS (MaskX).
+#ifndef NR_FWD_W2
+#define NR_FWD_W2 0
+#endif
+#if NR_FWD_W2 && !NR_F16
+#error "NR_FWD_W2 is an f16x3 variant"
+#endif
+#if NR_FWD_W2
+#define NR_X3_WAVES 8
+#endif
 #include "x3.h"
 
 namespace {
@@ -35,7 +50,12 @@ constexpr int kHeadLds = kHeadDma * 1024;
 #endif
 constexpr int kPeQ = 12;                          // float4 per lane: xyz PE slots (8), dir PE (4)
 constexpr int kPeBytes = NR_PE_REGS ? 0 : kWaves * kPeQ * 64 * 16;  // each wave's encodings, parked for layer 5 / dir
-constexpr int kLdsBytes = kRingBytes + kHeadLds + kPeBytes;
+constexpr int kNS = NR_FWD_W2 ? 1 : 2;            // 16-sample tiles per wave
+constexpr int kBlocks = kWaves * kNS / 2;         // 32-sample blocks per workgroup
+static_assert(NR_PE_REGS || kNS == 2, "encodings parked in LDS: two tiles per wave only");
+constexpr int kXchBytes = kNS == 1 ? kWaves * 2 * 64 * 16 : 0;   // MaskX slots
+constexpr int kLdsBytes = kRingBytes + kHeadLds + kPeBytes + kXchBytes;
+static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
 // ---- the k-group sequence (packing.py FWD3_LAYERS) --------------------------
 constexpr int kL1 = 0, kL2 = 4, kL3 = 20, kL4 = 36, kL5 = 52, kL6 = 72, kL7 = 88, kL8 = 104;
@@ -55,21 +75,21 @@ struct FwdTab {
 static_assert(FwdTab::off(kQAll) == (NR_F16 ? 2388000 : (NR_BF1 ? 1200160 : 3575840)),
               "packed size must match packing.fwd3_offsets()");
 
-// w . relu(x) for both sample tiles, reduced over the 4 lane groups
-template <bool RELU, int NF>
-__device__ __forceinline__ void head_dot(const f32x4 (&acc)[NF][2], const float* __restrict__ w,
+// w . relu(x) for the wave's sample tiles, reduced over the 4 lane groups
+template <bool RELU, int NF, int NS>
+__device__ __forceinline__ void head_dot(const f32x4 (&acc)[NF][NS], const float* __restrict__ w,
                                          int g, float (&p)[2]) {
     p[0] = p[1] = 0.f;
 #pragma unroll
     for (int F = 0; F < NF; ++F) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(w + 16 * F + 4 * g);
 #pragma unroll
-        for (int S = 0; S < 2; ++S)
+        for (int S = 0; S < NS; ++S)
 #pragma unroll
             for (int r = 0; r < 4; ++r) p[S] = fmaf(RELU ? relu_i(acc[F][S][r]) : acc[F][S][r], v[r], p[S]);
     }
 #pragma unroll
-    for (int S = 0; S < 2; ++S) p[S] = sum_over_groups(p[S]);
+    for (int S = 0; S < NS; ++S) p[S] = sum_over_groups(p[S]);
 }
 
 // xyz positional encoding in the slot order of packing.PE16_MAP: lane group g
@@ -154,22 +174,60 @@ __device__ __forceinline__ void store_pe4(const float* v, int s, int jh, int S, 
 
 struct MaskWords { uint32_t w[4] = {0u, 0u, 0u, 0u}; };
 
+// A block's ReLU mask words (layout.h: lane word F >> 2, bit 8 (F & 3) + 4 S + r)
+// hold both sample tiles' bits.  With one tile per wave (kNS = 1) each wave
+// publishes its words of layer l in its LDS slot l & 1 when the layer is
+// complete, and the block's even wave, one layer later (ring barriers in
+// between), ORs the pair's words of layer l - 1 and stores them; the last
+// layer is stored after a workgroup barrier (last()).  kNS = 2 stores directly.
+struct MaskX {
+    uint4* lds;        // this wave's two slots of 64 uint4 (the partner's follow it)
+    uint32_t* base;    // the block's mask segment (layer l at + 256 l)
+    int lane;
+    bool even;
+    __device__ __forceinline__ void flush(int l) const {
+        const uint4 a = lds[(l & 1) * 64 + lane], b = lds[128 + (l & 1) * 64 + lane];
+        *reinterpret_cast<uint4*>(base + l * 256 + lane * 4) =
+            make_uint4(a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w);
+    }
+    __device__ __forceinline__ void put(int l, const uint32_t (&w)[4]) const {
+        if constexpr (kNS == 2) {
+            *reinterpret_cast<uint4*>(base + l * 256 + lane * 4) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            lds[(l & 1) * 64 + lane] = make_uint4(w[0], w[1], w[2], w[3]);
+            if (l > 0 && even) flush(l - 1);
+        }
+    }
+    // after the last put(l): the block's words of layer l
+    __device__ __forceinline__ void last(int l) const {
+        if constexpr (kNS == 1) {
+            __syncthreads();
+            if (even) flush(l);
+        }
+    }
+};
+
 enum FwdMode { FWD_RAYS = 0, FWD_EMB = 1, FWD_PTS = 2 };
 
 // layer 1's side: the xyz PE slots saved, 2 float4 per group (tiles 2, 6)
 template <bool SAVE, bool ROWS>
 struct PeSide {
-    // stores at tiles 2 and 6
-    static constexpr int before(int T) { return SAVE ? (T > 2) + (T > 6) : 0; }
-    const float (&pe)[2][16];
+    // stores at tiles 2 and 6 (one tile per wave: at tile 2)
+    static constexpr int before(int T) { return SAVE ? (T > 2) + (kNS == 2 && T > 6) : 0; }
+    const float (&pe)[kNS][16];
     float* dst;
-    int g, lane;
+    int g, lane, s0;
     template <typename GC>
     __device__ __forceinline__ void operator()(GC, int t) const {
-        if constexpr (SAVE) {
+        if constexpr (SAVE && kNS == 2) {
             if (t == 2 || t == 6) {
                 const int u = 2 * GC::value + (t == 6), S = u >> 2, s = (u >> 1) & 1, jh = u & 1;
                 store_pe4<64, ROWS>(&pe[S][8 * s + 4 * jh], s, jh, S, g, dst, lane);
+            }
+        } else if constexpr (SAVE) {
+            if (t == 2) {
+                const int u = GC::value, s = u >> 1, jh = u & 1;
+                store_pe4<64, ROWS>(&pe[0][8 * s + 4 * jh], s, jh, s0, g, dst, lane);
             }
         }
     }
@@ -178,17 +236,22 @@ struct PeSide {
 // the dir layer's PE part: the dir PE slots saved N16 at tiles 1, 3, 5, 7
 template <bool SAVE>
 struct DirPeSide {
-    // stores at the odd tiles
-    static constexpr int before(int T) { return SAVE ? T / 2 : 0; }
-    const float (&dpe)[2][8];
+    // stores at the odd tiles (one tile per wave: at tiles 1 and 5)
+    static constexpr int before(int T) { return SAVE ? (kNS == 2 ? T / 2 : (T > 1) + (T > 5)) : 0; }
+    const float (&dpe)[kNS][8];
     float* dst;
-    int g, lane;
+    int g, lane, s0;
     template <typename GC>
     __device__ __forceinline__ void operator()(GC, int t) const {
-        if constexpr (SAVE) {
+        if constexpr (SAVE && kNS == 2) {
             if (t & 1) {
                 const int u = t >> 1;
                 store_pe4<32, true>(&dpe[u >> 1][4 * (u & 1)], 0, u & 1, u >> 1, g, dst, lane);
+            }
+        } else if constexpr (SAVE) {
+            if (t == 1 || t == 5) {
+                const int h = t >> 2;
+                store_pe4<32, true>(&dpe[0][4 * h], 0, h, s0, g, dst, lane);
             }
         }
     }
@@ -216,11 +279,13 @@ struct AccU {
     static constexpr bool kStores = STORE;
     static constexpr bool kPaired = STORE && ROWS && kRowPair;
     template <typename P> __device__ __forceinline__ void begin(const P&) {}
-    const f32x4 (&X)[16][2];
+    const f32x4 (&X)[16][kNS];
     float* dst;
-    uint32_t* msk;
+    uint32_t* msk;     // MASK: the layer's mask words (kNS = 2)
+    const MaskX* mx;   // ... or their exchange (kNS = 1), and the layer
+    int ml;
     const float* wsig;
-    int lane, g;
+    int lane, g, s0;
     float pend[2] = {0.f, 0.f};
     f32x4 held = {0.f, 0.f, 0.f, 0.f};   // kPaired: the even tile, stored with the odd one
     uint32_t w[4] = {0u, 0u, 0u, 0u};
@@ -259,18 +324,23 @@ struct AccU {
             } else {
                 const int F = 2 * s + (p >> 1);
                 const f32x4 v = {pend[0], pend[1], x0, x1};
+                const int S = (kNS == 2 ? 0 : s0) + sb;     // the block's tile
                 if constexpr (kPaired) {
                     if (p == 1) held = v;
-                    else store_row_pair<256>(held, v, 2 * s, sb, dst, lane);
+                    else store_row_pair<256>(held, v, 2 * s, S, dst, lane);
                 } else if constexpr (ROWS) {
-                    store_row<256>(v, F, sb, dst, lane);
+                    store_row<256>(v, F, S, dst, lane);
                 } else {
-                    store_n16(v, F, sb, dst, lane);
+                    store_n16(v, F, S, dst, lane);
                 }
                 if constexpr (MASK) {
-                    mask_bits(v, F, sb, w);
-                    if (s == 7 && sb == 1 && p == 3)
-                        *reinterpret_cast<uint4*>(msk + lane * 4) = make_uint4(w[0], w[1], w[2], w[3]);
+                    mask_bits(v, F, S, w);
+                    if (s == 7 && sb == kNS - 1 && p == 3) {
+                        if constexpr (kNS == 2)
+                            *reinterpret_cast<uint4*>(msk + lane * 4) = make_uint4(w[0], w[1], w[2], w[3]);
+                        else
+                            mx->put(ml, w);
+                    }
                 }
             }
         }
@@ -283,7 +353,7 @@ struct PeU {
     static constexpr bool kStores = false;
     static constexpr bool kPaired = false;
     template <typename P> __device__ __forceinline__ void begin(const P&) {}
-    const float (&pe)[2][N];
+    const float (&pe)[kNS][N];
     template <typename SC>
     __device__ __forceinline__ void operator()(SC, int sb, int p, float& x0, float& x1) const {
         constexpr int s = SC::value;
@@ -308,7 +378,7 @@ template <int S = 0, typename GetU>
 __device__ __forceinline__ void drain_all(GetU& u) {
     if constexpr (S < 8) {
 #pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
+        for (int sb = 0; sb < kNS; ++sb)
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
                 float x0, x1;
@@ -333,14 +403,16 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4;
-    const int blk = blockIdx.x * kWaves + wave;
+    const int wb = kNS == 2 ? wave : wave >> 1;   // the wave's block within the workgroup
+    const int s0 = kNS == 2 ? 0 : wave & 1;       // the block's first tile this wave holds
+    const int blk = blockIdx.x * kBlocks + wb;
     const int m = LIST ? __builtin_amdgcn_readfirstlane(*a.scount) : a.n;
-    if (LIST && (int)blockIdx.x * kWaves * 32 >= m) return;   // whole workgroup: before any barrier
+    if (LIST && (int)blockIdx.x * kBlocks * 32 >= m) return;   // whole workgroup: before any barrier
     int smp[2];
     bool valid[2];
 #pragma unroll
-    for (int S = 0; S < 2; ++S) {
-        const int s_raw = blk * 32 + 16 * S + (lane & 15);
+    for (int S = 0; S < kNS; ++S) {
+        const int s_raw = blk * 32 + 16 * (s0 + S) + (lane & 15);
         valid[S] = s_raw < m;
         if constexpr (LIST) smp[S] = a.slist[valid[S] ? s_raw : 0];
         else smp[S] = valid[S] ? s_raw : a.n - 1;
@@ -353,10 +425,10 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 
     // sample inputs first: they are waited for while the weight DMA below
     // stays in flight (vmcnt retires in issue order)
-    float pe[2][16], dg[2][8];
-    float in[2][7];
+    float pe[kNS][16], dg[kNS][8];
+    float in[kNS][7];
 #pragma unroll
-    for (int S = 0; S < 2; ++S) {
+    for (int S = 0; S < kNS; ++S) {
         const int s = smp[S];
         if constexpr (EMB) {
             pe_gather(pe[S], a.x + (size_t)s * a.xstride, g);
@@ -391,7 +463,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     [[maybe_unused]] f32x4* pe_lds =
         reinterpret_cast<f32x4*>(smem + kRingBytes + kHeadLds) + wave * kPeQ * 64 + lane;
 #pragma unroll
-    for (int S = 0; S < 2; ++S) {
+    for (int S = 0; S < kNS; ++S) {
         if constexpr (MODE == FWD_PTS) {
             pe_encode(pe[S], in[S][0], in[S][1], in[S][2], g);
         } else if constexpr (MODE == FWD_RAYS) {
@@ -423,8 +495,8 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     enter<FwdTab, 0, QEND>(smem, lane, f0);
     NR_STAMP(1);       // prologue: + first weight group
 
-    Act A, B;
-    Pieces b[2];       // pieces of the next k-step
+    ActN<kNS> A, B;
+    Pieces b[kNS];     // pieces of the next k-step
     auto hseg = [&](int l) { return SV + nr_sv_h(l, nb) + (size_t)blk * NR_SEGF(256); };
     auto mseg = [&](int l) {
         return reinterpret_cast<uint32_t*>(SV + nr_sv_mask(nb)) + ((size_t)blk * NR_MASK_LAYERS + l) * 256;
@@ -437,27 +509,29 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     // (wgrad.hip reads each as its task list expects)
     constexpr bool kRows = !SIGMA_ONLY;
     using U = AccU<true, SAVE, SAVE, false, kRows>;
+    const MaskX mx{reinterpret_cast<uint4*>(smem + kRingBytes + kHeadLds + kPeBytes) + 128 * wave,
+                   mseg(0), lane, s0 == 0};
 
     // layer 1: PE(63) -> 256; stores the PE slots
     PeU<16> peu{pe};
     split_all(peu, b);
-    U u1{A, hseg(0), mseg(0), nullptr, lane, g};
+    U u1{A, hseg(0), mseg(0), &mx, 0, nullptr, lane, g, s0};
     {
-        PeSide<SAVE, kRows> side{pe, SV + (size_t)blk * NR_SEGF(64), g, lane};
+        PeSide<SAVE, kRows> side{pe, SV + (size_t)blk * NR_SEGF(64), g, lane, s0};
         auto bi = bias(NR_H_BIAS(1));
         segment<FwdTab, kL1, 2, 2, QEND, true>(dma, lane, A, peu, u1, bi, side, b, f0);
     }
     NR_STAMP(2);
-    U u2{B, hseg(1), mseg(1), nullptr, lane, g};
+    U u2{B, hseg(1), mseg(1), &mx, 1, nullptr, lane, g, s0};
     { auto bi = bias(NR_H_BIAS(2)); segment<FwdTab, kL2, 8, 2, QEND, true>(dma, lane, B, u1, u2, bi, none, b, f0); }
     NR_STAMP(3);
-    U u3{A, hseg(2), mseg(2), nullptr, lane, g};
+    U u3{A, hseg(2), mseg(2), &mx, 2, nullptr, lane, g, s0};
     { auto bi = bias(NR_H_BIAS(3)); segment<FwdTab, kL3, 8, 2, QEND, true>(dma, lane, A, u2, u3, bi, none, b, f0); }
     NR_STAMP(4);
-    float pe5[2][16];
+    float pe5[kNS][16];
 #if NR_PE_REGS
 #pragma unroll
-    for (int S = 0; S < 2; ++S)
+    for (int S = 0; S < kNS; ++S)
 #pragma unroll
         for (int i = 0; i < 16; ++i) pe5[S][i] = pe[S][i];
 #else
@@ -472,22 +546,22 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
     { auto bi = bias(NR_H_BIAS(4)); segment<FwdTab, kL4, 8, 2, QEND, true>(dma, lane, B, u3, pe5u, bi, none, b, f0); }
     NR_STAMP(5);
     // layer 5: cat[PE, h4] -> 256 (nerf.py:108-109)
-    U u4{B, hseg(3), mseg(3), nullptr, lane, g};
+    U u4{B, hseg(3), mseg(3), &mx, 3, nullptr, lane, g, s0};
     { auto bi = bias(NR_H_BIAS(5)); segment<FwdTab, kL5, 2, 2, QEND, true>(dma, lane, A, pe5u, u4, bi, none, b, f0); }
     NR_STAMP(6);
-    U u5{A, hseg(4), mseg(4), nullptr, lane, g};
+    U u5{A, hseg(4), mseg(4), &mx, 4, nullptr, lane, g, s0};
     segment<FwdTab, kL5 + 4, 8, 2, QEND, false>(dma, lane, A, u4, u5, zero, none, b, f0);
     NR_STAMP(7);
-    U u6{B, hseg(5), mseg(5), nullptr, lane, g};
+    U u6{B, hseg(5), mseg(5), &mx, 5, nullptr, lane, g, s0};
     { auto bi = bias(NR_H_BIAS(6)); segment<FwdTab, kL6, 8, 2, QEND, true>(dma, lane, B, u5, u6, bi, none, b, f0); }
     NR_STAMP(8);
-    U u7{A, hseg(6), mseg(6), nullptr, lane, g};
+    U u7{A, hseg(6), mseg(6), &mx, 6, nullptr, lane, g, s0};
     { auto bi = bias(NR_H_BIAS(7)); segment<FwdTab, kL7, 8, 2, QEND, true>(dma, lane, A, u6, u7, bi, none, b, f0); }
     NR_STAMP(9);
 
-    // lane group g < 2 writes sample tile S = g
-    const int Sw = g & 1;
-    const bool wr = g < 2 && valid[Sw];
+    // lane group g < kNS writes the wave's sample tile g
+    const int Sw = kNS == 2 ? (g & 1) : 0;
+    const bool wr = g < kNS && valid[Sw];
     const int sw = smp[Sw];
     if constexpr (SIGMA_ONLY && SAVE) {
         // training a sigma-only graph (rendering_shadows.py:167, the shadow
@@ -496,12 +570,13 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         // splitting h8 for xyz_encoding_final, and sigma comes from the same
         // sums; out rows are (n, 4) [0, 0, 0, sigma] for the backward's contract
         { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, nonext, bi, none, b, f0); }
-        AccU<true, true, true, true, false> u8{B, hseg(7), mseg(7), H + NR_H_WSIG, lane, g};
+        AccU<true, true, true, true, false> u8{B, hseg(7), mseg(7), &mx, 7, H + NR_H_WSIG, lane, g, s0};
         u8.preload();
         drain_all(u8);
+        mx.last(7);
         float sigma[2];
 #pragma unroll
-        for (int S = 0; S < 2; ++S) {
+        for (int S = 0; S < kNS; ++S) {
             sigma[S] = sum_over_groups(u8.sig[S]) + H[NR_H_BSIG];
         }
         if (wr && !LIST)
@@ -515,15 +590,15 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         return;
     } else {
         // h8 feeds xyz_encoding_final and, while it is split, the sigma head
-        AccU<true, SAVE, SAVE, true> u8{B, hseg(7), mseg(7), H + NR_H_WSIG, lane, g};
+        AccU<true, SAVE, SAVE, true> u8{B, hseg(7), mseg(7), &mx, 7, H + NR_H_WSIG, lane, g, s0};
         u8.preload();
         { auto bi = bias(NR_H_BIAS(8)); segment<FwdTab, kL8, 8, 2, QEND, true>(dma, lane, B, u7, u8, bi, none, b, f0); }
         NR_STAMP(10);
         // dir_encoding: ReLU(Linear(283,128)(cat[feat, PE(dir)])) (nerf.py:118-119)
-        float dpe[2][8];
+        float dpe[kNS][8];
 #if NR_PE_REGS
 #pragma unroll
-        for (int S = 0; S < 2; ++S)
+        for (int S = 0; S < kNS; ++S)
 #pragma unroll
             for (int i = 0; i < 8; ++i) dpe[S][i] = dg[S][i];
 #else
@@ -541,18 +616,18 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         // not saved: the weight gradient of the dir layer's feat columns is
         // formed from h8 (wgrad.hip task 10, nr_wgrad_dir_feat) -- 1 KiB per
         // sample fewer stores, and the densest store phase of the kernel gone
-        AccU<false, false, false, false> uf{A, nullptr, nullptr, nullptr, lane, g};
+        AccU<false, false, false, false> uf{A, nullptr, nullptr, nullptr, 0, nullptr, lane, g, s0};
         { auto bi = bias(NR_H_BFINAL); segment<FwdTab, kFinal, 8, 2, QEND, true>(dma, lane, A, u8, uf, bi, none, b, f0); }
         NR_STAMP(11);
         float sigma[2];
 #pragma unroll
-        for (int S = 0; S < 2; ++S) {
+        for (int S = 0; S < kNS; ++S) {
             sigma[S] = sum_over_groups(u8.sig[S]) + H[NR_H_BSIG];
         }
-        f32x4 C[8][2];
+        f32x4 C[8][kNS];
         { auto bi = bias(NR_H_BDIR); segment<FwdTab, kDir, 8, 1, QEND, true>(dma, lane, C, uf, dpeu, bi, none, b, f0); }
         {   // PE(dir) part (stores the dir PE slots)
-            DirPeSide<SAVE> side{dpe, SV + nr_sv_dirpe(nb) + (size_t)blk * NR_SEGF(32), g, lane};
+            DirPeSide<SAVE> side{dpe, SV + nr_sv_dirpe(nb) + (size_t)blk * NR_SEGF(32), g, lane, s0};
             segment<FwdTab, kDir + 8, 1, 1, QEND, false>(dma, lane, C, dpeu, nonext, zero, side, b, f0);
         }
         NR_STAMP(12);
@@ -571,7 +646,7 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
         }
 #if NR_X3_DBG == 8
         if (lane == 0) {
-            uint64_t* st = reinterpret_cast<uint64_t*>(a.out) + (size_t)blk * 16;
+            uint64_t* st = reinterpret_cast<uint64_t*>(a.out) + (size_t)(blockIdx.x * kWaves + wave) * 16;
             st[0] = r0;
             st[1] = __builtin_amdgcn_s_memrealtime();
             st[2] = __builtin_amdgcn_s_memtime() - t0;
@@ -584,14 +659,19 @@ __global__ void __launch_bounds__(64 * kWaves, 1) mlp_fwd3_kernel(Fwd3Args a) {
 #pragma unroll
             for (int F = 0; F < 8; ++F)
 #pragma unroll
-                for (int S = 0; S < 2; ++S) {
+                for (int S = 0; S < kNS; ++S) {
                     f32x4 v = C[F][S];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] = relu_i(v[r]) * kWUnscale;
-                    store_row<128>(v, F, S, hd, lane);
-                    mask_bits(v, F, S, w);
+                    store_row<128>(v, F, s0 + S, hd, lane);
+                    mask_bits(v, F, s0 + S, w);
                 }
-            *reinterpret_cast<uint4*>(mseg(8) + lane * 4) = make_uint4(w[0], w[1], w[2], w[3]);
+            if constexpr (kNS == 2) {
+                *reinterpret_cast<uint4*>(mseg(8) + lane * 4) = make_uint4(w[0], w[1], w[2], w[3]);
+            } else {
+                mx.put(8, w);
+                mx.last(8);
+            }
         }
     }
 }
@@ -672,7 +752,7 @@ NR_API int NR_X3_NAME(nr_mlp_fwd)(const void* packed, const float* rays, const f
                "nr_mlp_fwd_x3: a sigma_only run keeps activations only on the ray path");
     Fwd3Args a{reinterpret_cast<const char*>(packed), nullptr, rays, z, x, (int)n,
                samples_per_ray, xstride, out, save};
-    const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
+    const int blocks = (int)((n + 32 * kBlocks - 1) / (32 * kBlocks));
     hipStream_t st = (hipStream_t)stream;
     const bool sv = save != nullptr;
     if (emb) {
@@ -706,7 +786,7 @@ NR_API int NR_X3_NAME(nr_mlp_fwd_listed)(const void* packed, const float* rays, 
                "nr_mlp_fwd_listed: packed/save must be 16-byte aligned");
     Fwd3Args a{reinterpret_cast<const char*>(packed), nullptr, rays, z, nullptr, (int)n,
                samples_per_ray, 0, nullptr, save, samples, count};
-    const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
+    const int blocks = (int)((n + 32 * kBlocks - 1) / (32 * kBlocks));
     hipStream_t st = (hipStream_t)stream;
     if (sigma_only) mlp_fwd3_kernel<FWD_RAYS, true, true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
     else mlp_fwd3_kernel<FWD_RAYS, false, true, true><<<blocks, 64 * kWaves, 0, st>>>(a);
@@ -723,7 +803,7 @@ NR_API int NR_X3_NAME(nr_mlp_sigma_points)(const void* packed, const float* pts,
     NR_REQUIRE(((uintptr_t)packed & 15) == 0, "nr_mlp_sigma_points_x3: packed alignment");
     Fwd3Args a{reinterpret_cast<const char*>(packed), pts, nullptr, nullptr, nullptr, (int)n, 1, 0,
                sigma_out, nullptr};
-    const int blocks = (int)((n + 32 * kWaves - 1) / (32 * kWaves));
+    const int blocks = (int)((n + 32 * kBlocks - 1) / (32 * kBlocks));
     mlp_fwd3_kernel<FWD_PTS, true, false><<<blocks, 64 * kWaves, 0, (hipStream_t)stream>>>(a);
     NR_LAUNCH_CHECK("nr_mlp_sigma_points_x3");
     return 0;

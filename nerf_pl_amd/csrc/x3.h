@@ -108,7 +108,13 @@ constexpr int kWScale = 0;
 // 2^-kWScale: takes a layer's accumulator (weights scaled) back to true values
 constexpr float kWUnscale = 1.0f / (float)(1 << kWScale);
 
-constexpr int kWaves = 4;
+// waves per workgroup sharing one weight ring.  A kernel may set it before
+// including this header (mlp_bwd3.hip's two-waves-per-SIMD form: 8 waves of
+// one 16-sample tile each); the DMA of a group is split over the waves.
+#ifndef NR_X3_WAVES
+#define NR_X3_WAVES 4
+#endif
+constexpr int kWaves = NR_X3_WAVES;
 constexpr int kTiles = 8;                          // output tiles (16 rows) per k-group
 // ring depth in k-groups: the DMA of group q is issued kSlots-1 groups before
 // q is consumed, and the wait for it also waits for every older store (vmcnt
@@ -120,6 +126,7 @@ constexpr int kTiles = 8;                          // output tiles (16 rows) per
 constexpr int kSlots = NR_X3_SLOTS;
 constexpr int kSlotBytes = kNP * kTiles * 1024;    // pieces x 8 tiles x 1 KiB
 constexpr int kDma = kNP * kTiles / kWaves;        // DMA instructions per wave per group
+static_assert(kDma * kWaves == kNP * kTiles, "a group's DMA must split evenly over the waves");
 // Merged ring (NR_X3_MERGE): the groups of one k-step (both output halves of a
 // 256-wide layer) share one ring slot of 2 groups and ONE hand-over (wait +
 // barrier) instead of one per group; the packed layout is unchanged (the two
@@ -145,7 +152,8 @@ constexpr int kRingBytes = kMerge ? kSS * kSuperBytes : kSlots * kSlotBytes;
 
 template <int V> using IC = std::integral_constant<int, V>;
 
-typedef f32x4 Act[16][2];                      // 256-wide activation of one wave
+typedef f32x4 Act[16][2];                      // 256-wide activation of one wave (two sample tiles)
+template <int NS> using ActN = f32x4[16][NS];  // ... of NS sample tiles
 
 // vm operations this wave issued after its DMA for group q by the time group
 // q is consumed: the DMA of the kSlots-2 groups after it (merged ring: of the
@@ -427,31 +435,33 @@ __device__ __forceinline__ f32x4 mfma16(const p8& a, const p8& b, f32x4 c) {
 #endif
 }
 
-// d[S] = c[S] + W * B[S] for both sample tiles: the piece products (bf16x6:
-// six of order <= 2^-16; f16x3: three of order <= 2^-11), small terms first,
-// the two accumulators alternating
-__device__ __forceinline__ void x6_pair(const Frag& w, const Pieces (&b)[2], f32x4 c0, f32x4 c1,
-                                        f32x4& d0, f32x4& d1) {
+// c[S] += W * B[S] for the wave's NS sample tiles: the piece products
+// (bf16x6: six of order <= 2^-16; f16x3: three of order <= 2^-11), small
+// terms first, the accumulators alternating
+template <int NS>
+__device__ __forceinline__ void x6_multi(const Frag& w, const Pieces (&b)[NS], f32x4 (&c)[NS]) {
     if constexpr (NR_X3_DBG == 4) {
-        asm volatile("" ::"v"(w.p[0]), "v"(w.p[kNP - 1]), "v"(b[0].hi), "v"(b[1].hi));
-        d0 = c0; d1 = c1;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) asm volatile("" ::"v"(w.p[0]), "v"(w.p[kNP - 1]), "v"(b[j].hi));
         return;
     }
+    auto prod = [&](const p8& a, auto piece) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) c[j] = mfma16(a, piece(b[j]), c[j]);
+    };
 #if NR_F16
-    c0 = mfma16(w.p[1], b[0].hi, c0);  c1 = mfma16(w.p[1], b[1].hi, c1);
-    c0 = mfma16(w.p[0], b[0].lo, c0);  c1 = mfma16(w.p[0], b[1].lo, c1);
-    d0 = mfma16(w.p[0], b[0].hi, c0);  d1 = mfma16(w.p[0], b[1].hi, c1);
-    return;
+    prod(w.p[1], [](const Pieces& x) { return x.hi; });
+    prod(w.p[0], [](const Pieces& x) { return x.lo; });
+    prod(w.p[0], [](const Pieces& x) { return x.hi; });
 #elif NR_BF1
-    d0 = mfma16(w.p[0], b[0].hi, c0);  d1 = mfma16(w.p[0], b[1].hi, c1);
-    return;
+    prod(w.p[0], [](const Pieces& x) { return x.hi; });
 #else
-    c0 = mfma16(w.p[2], b[0].hi, c0);  c1 = mfma16(w.p[2], b[1].hi, c1);
-    c0 = mfma16(w.p[0], b[0].lo, c0);  c1 = mfma16(w.p[0], b[1].lo, c1);
-    c0 = mfma16(w.p[1], b[0].mid, c0); c1 = mfma16(w.p[1], b[1].mid, c1);
-    c0 = mfma16(w.p[1], b[0].hi, c0);  c1 = mfma16(w.p[1], b[1].hi, c1);
-    c0 = mfma16(w.p[0], b[0].mid, c0); c1 = mfma16(w.p[0], b[1].mid, c1);
-    d0 = mfma16(w.p[0], b[0].hi, c0);  d1 = mfma16(w.p[0], b[1].hi, c1);
+    prod(w.p[2], [](const Pieces& x) { return x.hi; });
+    prod(w.p[0], [](const Pieces& x) { return x.lo; });
+    prod(w.p[1], [](const Pieces& x) { return x.mid; });
+    prod(w.p[1], [](const Pieces& x) { return x.hi; });
+    prod(w.p[0], [](const Pieces& x) { return x.mid; });
+    prod(w.p[0], [](const Pieces& x) { return x.hi; });
 #endif
 }
 
@@ -475,15 +485,42 @@ struct BiasInit {     // bias[16F + 4g .. +3] (LDS), the same for both sample ti
 // holds tiles 0 .. kPF-1 of group Q+1.  hook(t) runs inside tile t; its VALU
 // work is interleaved with the tile's 2 kNProd MFMAs.  EXTRA: the stores the
 // hooks issue before the hand-over tile (left in flight by its vmcnt wait).
-template <class TAB, int Q, int QEND, int F0, bool INIT, int EXTRA, typename CInit, typename Hook, int NF>
-__device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][2],
-                                         const Pieces (&b)[2], CInit& cinit, Hook& hook, Ahead& a) {
+// Accumulators of a tile in AGPRs ("a") or VGPRs ("v"); at two waves per SIMD
+// a wave has 256 registers in all, so the split is the compiler's
+#ifndef NR_X3_ACC_AGPR
+#define NR_X3_ACC_AGPR 1
+#endif
+template <int NS>
+__device__ __forceinline__ void pin_acc(f32x4 (&d)[NS]) {
+#if NR_X3_ACC_AGPR
+    if constexpr (NS == 2) {     // one statement for the pair (the round-5 register assignment)
+        asm volatile("" : "+a"(d[0]), "+a"(d[1]));
+        return;
+    }
+#endif
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+#if NR_X3_ACC_AGPR
+        asm volatile("" : "+a"(d[j]));
+#else
+        asm volatile("" : "+v"(d[j]));
+#endif
+    }
+}
+
+template <class TAB, int Q, int QEND, int F0, bool INIT, int EXTRA, typename CInit, typename Hook, int NF,
+          int NS>
+__device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][NS],
+                                         const Pieces (&b)[NS], CInit& cinit, Hook& hook, Ahead& a) {
     constexpr int NR = kPF + 1;       // fragment sets in registers
     Frag f[NR];
 #pragma unroll
     for (int i = 0; i < kPF; ++i) f[i] = a.f[i];
-    f32x4 ci[2][2];
-    if constexpr (INIT) { ci[0][0] = cinit(F0, 0); ci[0][1] = cinit(F0, 1); }
+    f32x4 ci[2][NS];
+    if constexpr (INIT) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) ci[0][j] = cinit(F0, j);
+    }
 #pragma unroll
     for (int t = 0; t < kTiles; ++t) {
         const int tn = t + kPF;
@@ -491,21 +528,26 @@ __device__ __forceinline__ void group_mm(char* ring, int lane, f32x4 (&acc)[NF][
         else if (tn == kTiles) enter<TAB, Q + 1, QEND, EXTRA>(ring, lane, a.f[0]);
         else if constexpr (Q + 1 < QEND) rd_frag<TAB, Q + 1>(ring, lane, tn - kTiles, a.f[tn - kTiles]);
         if constexpr (INIT) {
-            if (t + 1 < kTiles) { ci[(t + 1) & 1][0] = cinit(F0 + t + 1, 0); ci[(t + 1) & 1][1] = cinit(F0 + t + 1, 1); }
+            if (t + 1 < kTiles) {
+#pragma unroll
+                for (int j = 0; j < NS; ++j) ci[(t + 1) & 1][j] = cinit(F0 + t + 1, j);
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
-        f32x4& d0 = acc[F0 + t][0];
-        f32x4& d1 = acc[F0 + t][1];
-        if constexpr (INIT) x6_pair(f[t % NR], b, ci[t & 1][0], ci[t & 1][1], d0, d1);
-        else x6_pair(f[t % NR], b, d0, d1, d0, d1);
+        f32x4 (&d)[NS] = acc[F0 + t];
+        if constexpr (INIT) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) d[j] = ci[t & 1][j];
+        }
+        x6_multi<NS>(f[t % NR], b, d);
         // keep the tile's MFMAs in this tile: MFMA intrinsics have no side
         // effects, so without an ordered use the instruction selector may
         // float them anywhere in the (huge) basic block
-        asm volatile("" : "+a"(d0), "+a"(d1));
+        pin_acc<NS>(d);
         hook(t);
 #if NR_X3_SGB
 #pragma unroll
-        for (int i = 0; i < 2 * kNProd; ++i) {
+        for (int i = 0; i < NS * kNProd; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, NR_X3_SGB, 0);  // VALU
         }
@@ -546,8 +588,8 @@ struct NoSide {
     template <typename T> __device__ __forceinline__ void operator()(T, int) const {}
 };
 
-template <typename GetU, int s>
-__device__ __forceinline__ void split_unit(GetU& getu, IC<s>, int u, Pieces (&bn)[2]) {
+template <typename GetU, int s, int NS>
+__device__ __forceinline__ void split_unit(GetU& getu, IC<s>, int u, Pieces (&bn)[NS]) {
     if constexpr (NR_X3_DBG == 5) return;
     const int sb = u >> 2, p = u & 3;
     float x0, x1;
@@ -556,10 +598,10 @@ __device__ __forceinline__ void split_unit(GetU& getu, IC<s>, int u, Pieces (&bn
     pin(bn[sb]);
 }
 
-template <typename GetU>
-__device__ __forceinline__ void split_all(GetU& getu, Pieces (&b)[2]) {
+template <typename GetU, int NS>
+__device__ __forceinline__ void split_all(GetU& getu, Pieces (&b)[NS]) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 4 * NS; ++u) {
         const int sb = u >> 2, p = u & 3;
         float x0, x1;
         getu(IC<0>(), sb, p, x0, x1);
@@ -567,25 +609,25 @@ __device__ __forceinline__ void split_all(GetU& getu, Pieces (&b)[2]) {
     }
 }
 
-// split unit u (= 4 S + p) run at tile t of half HF: NH = 2 spreads the 8
-// units over tiles 3..6 of both halves (the last k-step's units read output
-// tiles 0, 1 of the layer, final after tiles 0, 1 of half 0); NH = 1 runs
-// one per tile
-template <int NH, int HF>
+// split unit u (= 4 S + p) run at tile t of half HF: NH = 2 spreads the 4 NS
+// units over tiles 3 .. 2 + 2 NS of both halves (the last k-step's units read
+// output tiles 0, 1 of the layer, final after tiles 0, 1 of half 0); NH = 1
+// runs one per tile
+template <int NH, int HF, int NS = 2>
 __host__ __device__ constexpr int unit_at(int t) {
-    if constexpr (NH == 1) return t;
-    else return t >= 3 && t <= 6 ? 4 * HF + t - 3 : -1;
+    if constexpr (NH == 1) return t < 4 * NS ? t : -1;
+    else return t >= 3 && t < 3 + 2 * NS ? 2 * NS * HF + t - 3 : -1;
 }
 // the tile whose start hands the next group over (x3.h group_mm)
 constexpr int kHandTile = kTiles - kPF;
 // stores a storing getter issues before the hand-over tile of its group: one
 // per odd unit, or (PAIRED: the two halves of a 128-B row line together, x3.h
 // store_row_pair) two per unit p = 3
-template <int NH, int HF, bool PAIRED = false>
+template <int NH, int HF, bool PAIRED = false, int NS = 2>
 __host__ __device__ constexpr int stores_before_hand() {
     int n = 0;
     for (int t = 0; t < kHandTile; ++t) {
-        const int u = unit_at<NH, HF>(t);
+        const int u = unit_at<NH, HF, NS>(t);
         if (u < 0) continue;
         if (PAIRED) n += (u & 3) == 3 ? 2 : 0;
         else n += u & 1;
@@ -594,15 +636,15 @@ __host__ __device__ constexpr int stores_before_hand() {
 }
 
 template <class TAB, int Q0, int S, int KS, int NH, int QEND, bool INIT, int HF, typename GetU,
-          typename NextU, typename CInit, typename Side, int NF>
-__device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)[NF][2], GetU& getu,
+          typename NextU, typename CInit, typename Side, int NF, int NS>
+__device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)[NF][NS], GetU& getu,
                                           NextU& nextu, CInit& cinit, Side& side,
-                                          const Pieces (&b)[2], Pieces (&bn)[2], Ahead& f0) {
+                                          const Pieces (&b)[NS], Pieces (&bn)[NS], Ahead& f0) {
     if constexpr (HF < NH) {
         constexpr int Q = Q0 + NH * S + HF;
         auto hook = [&](int t) {
             if (t < kDma) dma_one<TAB, dma_target<TAB, Q, QEND>(), QEND>(dma, t);
-            const int u = unit_at<NH, HF>(t);
+            const int u = unit_at<NH, HF, NS>(t);
             if (u >= 0) {
                 if constexpr (S + 1 < KS) split_unit(getu, IC<S + 1>(), u, bn);
                 else if constexpr (!IsNoNext<NextU>::value) {
@@ -614,7 +656,7 @@ __device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)
         };
         constexpr bool ust = S + 1 < KS ? GetU::kStores : NextU::kStores;
         constexpr bool upr = S + 1 < KS ? GetU::kPaired : NextU::kPaired;
-        constexpr int extra = (ust ? stores_before_hand<NH, HF, upr>() : 0) + Side::before(kHandTile);
+        constexpr int extra = (ust ? stores_before_hand<NH, HF, upr, NS>() : 0) + Side::before(kHandTile);
         group_mm<TAB, Q, QEND, 8 * HF, INIT && S == 0, extra>(dma.ring, lane, acc, b, cinit, hook, f0);
         seg_group<TAB, Q0, S, KS, NH, QEND, INIT, HF + 1>(dma, lane, acc, getu, nextu, cinit, side,
                                                           b, bn, f0);
@@ -622,15 +664,15 @@ __device__ __forceinline__ void seg_group(const Dma& dma, int lane, f32x4 (&acc)
 }
 
 template <class TAB, int Q0, int S, int KS, int NH, int QEND, bool INIT, typename GetU,
-          typename NextU, typename CInit, typename Side, int NF>
-__device__ __forceinline__ void seg_from(const Dma& dma, int lane, f32x4 (&acc)[NF][2], GetU& getu,
+          typename NextU, typename CInit, typename Side, int NF, int NS>
+__device__ __forceinline__ void seg_from(const Dma& dma, int lane, f32x4 (&acc)[NF][NS], GetU& getu,
                                          NextU& nextu, CInit& cinit, Side& side,
-                                         Pieces (&b)[2], Ahead& f0) {
+                                         Pieces (&b)[NS], Ahead& f0) {
     if constexpr (S < KS) {
-        Pieces bn[2];
+        Pieces bn[NS];
         seg_group<TAB, Q0, S, KS, NH, QEND, INIT, 0>(dma, lane, acc, getu, nextu, cinit, side, b, bn, f0);
-        b[0] = bn[0];
-        b[1] = bn[1];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) b[j] = bn[j];
         seg_from<TAB, Q0, S + 1, KS, NH, QEND, INIT>(dma, lane, acc, getu, nextu, cinit, side, b, f0);
     }
 }
@@ -638,16 +680,16 @@ __device__ __forceinline__ void seg_from(const Dma& dma, int lane, f32x4 (&acc)[
 // b: on entry the pieces of this segment's k-step 0, on exit those of the
 // next segment's k-step 0 (split by nextu)
 template <class TAB, int Q0, int KS, int NH, int QEND, bool INIT, typename GetU, typename NextU,
-          typename CInit, typename Side, int NF>
-__device__ __forceinline__ void segment(const Dma& dma, int lane, f32x4 (&acc)[NF][2], GetU& getu,
-                                        NextU& nextu, CInit& cinit, Side& side, Pieces (&b)[2],
+          typename CInit, typename Side, int NF, int NS>
+__device__ __forceinline__ void segment(const Dma& dma, int lane, f32x4 (&acc)[NF][NS], GetU& getu,
+                                        NextU& nextu, CInit& cinit, Side& side, Pieces (&b)[NS],
                                         Ahead& f0) {
     seg_from<TAB, Q0, 0, KS, NH, QEND, INIT>(dma, lane, acc, getu, nextu, cinit, side, b, f0);
 }
 
 // B fragment element of k-step s from an accumulator input (packing.kmap16)
-template <int NF>
-__device__ __forceinline__ float acc_b(const f32x4 (&X)[NF][2], int s, int sb, int j) {
+template <int NF, int NS>
+__device__ __forceinline__ float acc_b(const f32x4 (&X)[NF][NS], int s, int sb, int j) {
     return X[2 * s + (j >> 2)][sb][j & 3];
 }
 
