@@ -74,6 +74,7 @@ def main():
         out[name] = {
             "samples_per_ray": S,
             "live_sample_fraction": float(first_dead.double().mean() / S),
+            "zero_weight_fraction": float((w == 0).double().mean()),
             "chunk_fraction_evaluated": float(chunks.double().mean() / math.ceil(S / 32)),
             "first_dead_quantiles": [int(x) for x in torch.quantile(first_dead.double(),
                                       torch.tensor([0.1, 0.25, 0.5, 0.75, 0.9], dtype=torch.double))],
