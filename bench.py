@@ -209,6 +209,10 @@ def parse():
     ap.add_argument("--noise-std", type=float, default=None,
                     help="opt.py --noise_std: std dev of the noise added to sigma")
     ap.add_argument("--lr", type=float, default=5e-4, help="opt.py --lr (Adam)")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="one optimizer step after the whole backward (no coarse/fine "
+                         "step pipelining, nerf_pl_amd/pipeline.py; env NR_BENCH_PIPELINE=0)")
+    ap.set_defaults(pipeline=os.environ.get("NR_BENCH_PIPELINE", "1") != "0")
     ap.add_argument("--chunk", type=int, default=32 * 1024,
                     help="opt.py --chunk: the batch is rendered in chunks of this many rays "
                          "(NeRFSystem.forward, train.py:49-71), one render_rays call each")
@@ -567,7 +571,7 @@ def wl_nerf_train(args, dev, rank, ndc):
         return cpu_train(args, budget, rays_all, name)
 
     return dict(name=name, metric=metric, workload=work, data=data, step=step, train=True,
-                models=models, rays_per_step=args.batch, samples_per_ray=S + I,
+                pipeline_ok=I > 0, models=models, rays_per_step=args.batch, samples_per_ray=S + I,
                 flop_per_ray=S * FLOP_TRAIN + (S + I) * FLOP_TRAIN, cpu=cpu)
 
 
@@ -772,10 +776,11 @@ def main():
     else:
         wl = wl_nerf_train(args, dev, rank, ndc=args.config == "cfg3")
 
-    opt, reducer = None, None
+    opt, reducer, pstep = None, None, None
     if wl["train"]:
         params = [p for m in wl["models"] for p in m.parameters()]
-        opt = FusedAdam(params, lr=args.lr, eps=1e-8)
+        if not (args.pipeline and wl.get("pipeline_ok")):
+            opt = FusedAdam(params, lr=args.lr, eps=1e-8)
         if use_dist:
             from nerf_pl_amd.distributed import GradAllReducer
             # one bucket per model: the fine model's all-reduce overlaps the
@@ -785,15 +790,36 @@ def main():
             # here, not inside the first gradient hook (autograd's thread)
             dist.barrier()
             progress("first collective done")
+        if opt is None:
+            # the coarse model's Adam and the next step's coarse pass beside
+            # the fine model's backward tail (nerf_pl_amd/pipeline.py)
+            from nerf_pl_amd.pipeline import PipelinedStep
+            pstep = PipelinedStep(wl["models"], lr=args.lr, eps=1e-8, reducer=reducer)
 
     first = [use_dist]
 
     def step():
+        from nerf_pl_amd import rendering as _r
+        if pstep is not None and _r.FINE_STREAM:
+            loss = pstep(wl["step"])
+            if first[0]:
+                torch.cuda.synchronize()
+                progress("first step (pipelined) done")
+            first[0] = False
+            return loss
         loss = wl["step"]()
         if first[0]:
             torch.cuda.synchronize()
             progress("first step: forward done")
-        if opt is not None:
+        if pstep is not None:    # the serialised pass: the same optimizers, one stream
+            pstep.opt_c.zero_grad(set_to_none=True)
+            pstep.opt_f.zero_grad(set_to_none=True)
+            loss.backward()
+            if reducer is not None:
+                reducer()
+            pstep.opt_c.step()
+            pstep.opt_f.step()
+        elif opt is not None:
             opt.zero_grad(set_to_none=True)
             loss.backward()
             if first[0]:

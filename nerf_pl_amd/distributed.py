@@ -95,22 +95,35 @@ class GradAllReducer:
         op = dist.ReduceOp.AVG if self._nccl() else dist.ReduceOp.SUM
         b.handle = dist.all_reduce(b.flat, op=op, group=self.group, async_op=True)
 
-    def __call__(self):
-        world = dist.get_world_size(self.group)
-        for b in self.buckets:
-            if b.handle is not None and b.stale:
-                b.handle.wait()
-                b.handle = None
-            if b.handle is None:
-                self._launch(b)
-        for b in self.buckets:
+    def _start(self, b):
+        if b.handle is not None and b.stale:
             b.handle.wait()
-            if not self._nccl():
-                b.flat.div_(world)
-            torch._foreach_copy_([p.grad for p in b.params], b.views)
-            b.seen.clear()
             b.handle = None
-            b.stale = False
+        if b.handle is None:
+            self._launch(b)
+
+    def _complete(self, b):
+        b.handle.wait()
+        if not self._nccl():
+            b.flat.div_(dist.get_world_size(self.group))
+        torch._foreach_copy_([p.grad for p in b.params], b.views)
+        b.seen.clear()
+        b.handle = None
+        b.stale = False
+
+    def __call__(self):
+        for b in self.buckets:
+            self._start(b)
+        for b in self.buckets:
+            self._complete(b)
+
+    def finish(self, i):
+        """Bucket i only: its averaged gradients into its parameters' ``.grad``,
+        ordered on the current stream (``pipeline.PipelinedStep`` finishes each
+        model's bucket on the stream of that model's optimizer step)."""
+        b = self.buckets[i]
+        self._start(b)
+        self._complete(b)
 
     def remove(self):
         """Detach the gradient hooks."""

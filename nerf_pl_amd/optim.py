@@ -4,7 +4,7 @@ weight_decay from opt.py).
 
 ``FusedAdam.step()`` updates every parameter tensor that has a gradient in
 ONE ``nr_adam_step`` launch (up to ``nr_adam_max_tensors()`` tensors per
-launch; the NeRF pair has 44), with torch's single-tensor Adam arithmetic.
+launch; the NeRF pair has 48), with torch's single-tensor Adam arithmetic.
 Parameters without a gradient are skipped, like torch.  State keys
 (``step``, ``exp_avg``, ``exp_avg_sq``) match torch's, so state dicts move
 between the two optimizers.

@@ -96,10 +96,12 @@ def test_grad_allreduce_matches_single_process(world):
         assert torch.all(ug == 0)
 
 
-def _bucket_worker(rank, world, port, q):
+def _bucket_worker(rank, world, port, q, per_bucket=False):
     """two models in separate buckets, reducer built before backward (the
     buckets launch from the gradient hooks); model b is used twice in the loss
-    and a second backward accumulates before the call (stale buckets)"""
+    and a second backward accumulates before the call (stale buckets).
+    per_bucket: each bucket finished on its own (GradAllReducer.finish, as
+    pipeline.PipelinedStep does), the coarse (first) bucket first"""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -115,7 +117,11 @@ def _bucket_worker(rank, world, port, q):
                 m.zero_grad(set_to_none=True)
             for _ in range(1 + it):          # it 1: two backward passes accumulate
                 _two_model_loss(ma, mb, x, y).backward()
-            red()
+            if per_bucket:
+                red.finish(0)
+                red.finish(1)
+            else:
+                red()
             # numpy: pickled by value (tensors would be shared through file
             # descriptors that die with this process)
             out.append([p.grad.numpy().copy() for p in list(ma.parameters()) + list(mb.parameters())])
@@ -136,12 +142,14 @@ def _two_model_loss(ma, mb, x, y):
     return ((ma(x) - y) ** 2).mean() + ((mb(x) + mb(2 * x) - y) ** 2).mean()
 
 
-def test_bucketed_allreduce_overlapped_from_hooks():
+@pytest.mark.parametrize("per_bucket", [False, True])
+def test_bucketed_allreduce_overlapped_from_hooks(per_bucket):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q, per_bucket))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [_to_t(q.get(timeout=120)) for _ in range(world)]
