@@ -785,7 +785,11 @@ def main():
             from nerf_pl_amd.distributed import GradAllReducer
             # one bucket per model: the fine model's all-reduce overlaps the
             # coarse model's backward
-            reducer = GradAllReducer(params, buckets=[list(m.parameters()) for m in wl["models"]])
+            # collectives issued after the backward is enqueued (hook_launch=False):
+            # one issued from a gradient hook held autograd's thread until its
+            # input was computed, serialising the two backward chains
+            reducer = GradAllReducer(params, buckets=[list(m.parameters()) for m in wl["models"]],
+                                     hook_launch=False)
             # first collective on the main thread: the communicator is set up
             # here, not inside the first gradient hook (autograd's thread)
             dist.barrier()
@@ -842,6 +846,8 @@ def main():
             if i == 0:
                 torch.cuda.synchronize()
                 progress(f"{what}: first warmup step done")
+        if pstep is not None:
+            pstep.flush()        # a deferred fine update (distributed path)
         if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
@@ -858,6 +864,8 @@ def main():
         t0 = time.perf_counter()
         for _ in range(steps):
             loss = step()
+        if pstep is not None:
+            pstep.flush()        # the last step's deferred fine update is part of it
         if use_dist:
             dist.barrier()
         torch.cuda.synchronize()

@@ -11,6 +11,7 @@ coarse model's backward.
 """
 from __future__ import annotations
 
+import contextlib
 import functools
 
 import hashlib
@@ -30,6 +31,8 @@ class _Bucket:
         self.seen = set()
         self.handle = None
         self.stale = False
+        self.ready = False
+        self.stream = None      # the stream its last gradient was accumulated on
 
 
 class GradAllReducer:
@@ -55,9 +58,22 @@ class GradAllReducer:
     reduces it again from the final gradients.  Every rank must run the same
     graph (the same buckets complete in the same order), as with DDP."""
 
-    def __init__(self, params, group=None, buckets=None):
+    def __init__(self, params, group=None, buckets=None, ordered=False, hook_launch=True):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
+        # ordered: the buckets' all-reduces are issued in bucket order (a ready
+        # bucket waits for the ones before it).  They share one RCCL stream, so
+        # issue order is execution order: pipeline.PipelinedStep finishes bucket
+        # 0 (the coarse model) for the next step's coarse pass, and must not find
+        # it queued behind bucket 1, whose gradients (the fine model's) the host
+        # reaches first but the GPU produces last.
+        self.ordered = ordered
+        # hook_launch=False: the hooks only note which buckets are complete and
+        # the collectives are issued by __call__ / finish, after the backward has
+        # been enqueued (DESIGN.md 15: an RCCL collective issued from inside the
+        # backward held the autograd thread until its input was computed, so the
+        # coarse chain was enqueued only after the fine one had finished)
+        self.hook_launch = hook_launch
         dev = self.params[0].device
         if buckets is None:
             groups = [self.params]
@@ -85,15 +101,30 @@ class GradAllReducer:
             return
         b.seen.add(id(p))
         if len(b.seen) == len(b.params):
-            self._launch(b)
+            b.ready = True
+            b.stream = torch.cuda.current_stream(p.device) if p.device.type == "cuda" else None
+            if not self.hook_launch:
+                return
+            if not self.ordered:
+                self._launch(b, b.stream)
+                return
+            for c in self.buckets:      # every ready bucket whose predecessors are issued
+                if c.handle is None:
+                    if not c.ready:
+                        break
+                    self._launch(c, c.stream)
 
-    def _launch(self, b):
-        for p in b.params:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-        torch.cat([p.grad.reshape(-1) for p in b.params], out=b.flat)
-        op = dist.ReduceOp.AVG if self._nccl() else dist.ReduceOp.SUM
-        b.handle = dist.all_reduce(b.flat, op=op, group=self.group, async_op=True)
+    def _launch(self, b, stream=None):
+        # from a hook: on the stream that accumulated the bucket's last gradient
+        # (a bucket issued from another bucket's hook runs there too); from
+        # __call__ / finish: on the caller's current stream
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            for p in b.params:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            torch.cat([p.grad.reshape(-1) for p in b.params], out=b.flat)
+            op = dist.ReduceOp.AVG if self._nccl() else dist.ReduceOp.SUM
+            b.handle = dist.all_reduce(b.flat, op=op, group=self.group, async_op=True)
 
     def _start(self, b):
         if b.handle is not None and b.stale:
@@ -110,6 +141,8 @@ class GradAllReducer:
         b.seen.clear()
         b.handle = None
         b.stale = False
+        b.ready = False
+        b.stream = None
 
     def __call__(self):
         for b in self.buckets:

@@ -25,7 +25,12 @@ model, and the two models' gradients and Adam updates are independent
 Every kernel reads exactly what it reads in the sequential schedule: the
 parameters after a step are bit-identical (tests/test_gpu_pipeline.py).
 With a ``GradAllReducer`` of one bucket per model (coarse first), each
-bucket's all-reduce is finished on the stream of its model's Adam.
+bucket's all-reduce is issued after the backward has been enqueued, on the
+stream of its model's Adam; the fine model's all-reduce and Adam are deferred
+to just before the next step's fine pass (``rendering.BEFORE_FINE``), because
+issuing an RCCL collective waits on the host for its input, and issued at the
+end of the step it would hold back the next step's coarse pass.  ``flush()``
+applies a deferred update (``__call__`` returns with one pending).
 """
 from __future__ import annotations
 
@@ -47,6 +52,12 @@ class PipelinedStep:
         self.opt_c = FusedAdam([p for p in models[0].parameters() if p.requires_grad], **kw)
         self.opt_f = FusedAdam([p for p in models[1].parameters() if p.requires_grad], **kw)
         self.reducer = reducer
+        if reducer is not None:
+            if len(reducer.buckets) != 2:
+                raise ValueError("PipelinedStep: the reducer needs one bucket per model, coarse first")
+            # collectives issued after the backward is enqueued, each model's
+            # on the stream of its Adam (GradAllReducer.hook_launch)
+            reducer.hook_launch = False
         dev = next(models[0].parameters()).device
         self.device = dev
         self.mains = [torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev)]
@@ -55,6 +66,7 @@ class PipelinedStep:
         self._coarse = [p for p in models[0].parameters() if p.requires_grad]
         self._n = 0
         self._ev = None
+        self._pending = None      # the deferred fine update (distributed path)
         self._hooks = [p.register_post_accumulate_grad_hook(self._accumulated) for p in self._coarse]
 
     def _accumulated(self, p):
@@ -78,8 +90,15 @@ class PipelinedStep:
             raise RuntimeError("PipelinedStep needs rendering.FINE_STREAM (the fine pass on its "
                                "own stream)")
         cur, nxt = self.mains[self.k & 1], self.mains[(self.k + 1) & 1]
+        if self._pending is not None:
+            rendering.BEFORE_FINE.append(self.flush)
         with torch.cuda.stream(cur):
             loss = loss_fn()
+        if self._pending is not None:      # loss_fn ran no fine pass
+            if self.flush in rendering.BEFORE_FINE:
+                rendering.BEFORE_FINE.remove(self.flush)
+            self.flush()
+        with torch.cuda.stream(cur):
             self.opt_c.zero_grad(set_to_none=True)
             self.opt_f.zero_grad(set_to_none=True)
             self._n, self._ev = 0, None
@@ -96,12 +115,22 @@ class PipelinedStep:
             if self.reducer is not None:
                 self.reducer.finish(0)
             self.opt_c.step()
-        with torch.cuda.stream(self.side):
-            if self.reducer is not None:
-                self.reducer.finish(1)
-            self.opt_f.step()
+        if self.reducer is None:
+            with torch.cuda.stream(self.side):
+                self.opt_f.step()
+        else:
+            self._pending = True
         self.k += 1
         return loss
+
+    def flush(self):
+        """the deferred fine update: its all-reduce and Adam on the side stream"""
+        if self._pending is None:
+            return
+        self._pending = None
+        with torch.cuda.stream(self.side):
+            self.reducer.finish(1)
+            self.opt_f.step()
 
     def remove(self):
         for h in self._hooks:

@@ -48,6 +48,14 @@ FINE_STREAM = os.environ.get("NERF_PL_AMD_FINE_STREAM", "1") != "0"
 FINE_STREAM_PRIORITY = int(os.environ.get("NERF_PL_AMD_FINE_STREAM_PRIORITY", "0"))
 
 
+# one-shot callables run right before the next fine pass is enqueued (after the
+# coarse pass): pipeline.PipelinedStep on the distributed path defers the fine
+# model's all-reduce and Adam there, so that issuing the collective -- which
+# waits on the host for the fine backward -- comes after the next step's
+# coarse pass has been enqueued
+BEFORE_FINE = []
+
+
 @functools.lru_cache(maxsize=None)
 def _side_stream(device_index: int):
     return torch.cuda.Stream(device=torch.device("cuda", device_index),
@@ -181,6 +189,8 @@ def render_rays(models, embeddings, rays, N_samples=64, use_disp=False, perturb=
             return composite_apply(raw_f, z_f, rays, noise_f, noise_std, seed, STREAM_NOISE_FINE,
                                    white_back)
 
+        while BEFORE_FINE:
+            BEFORE_FINE.pop(0)()
         if FINE_STREAM and torch.is_grad_enabled() and any(
                 p.requires_grad for p in models[1].parameters()):
             main = torch.cuda.current_stream(dev)

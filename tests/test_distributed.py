@@ -101,7 +101,8 @@ def _bucket_worker(rank, world, port, q, per_bucket=False):
     buckets launch from the gradient hooks); model b is used twice in the loss
     and a second backward accumulates before the call (stale buckets).
     per_bucket: each bucket finished on its own (GradAllReducer.finish, as
-    pipeline.PipelinedStep does), the coarse (first) bucket first"""
+    pipeline.PipelinedStep does), the coarse (first) bucket first, the
+    all-reduces issued in bucket order (ordered=True)"""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -109,7 +110,8 @@ def _bucket_worker(rank, world, port, q, per_bucket=False):
         from nerf_pl_amd.distributed import GradAllReducer
         ma, mb, x_all, y_all = _two_models()
         red = GradAllReducer(list(ma.parameters()) + list(mb.parameters()),
-                             buckets=[list(ma.parameters()), list(mb.parameters())])
+                             buckets=[list(ma.parameters()), list(mb.parameters())],
+                             ordered=per_bucket)
         x, y = x_all[rank::world], y_all[rank::world]
         out = []
         for it in range(2):

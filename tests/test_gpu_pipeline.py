@@ -9,7 +9,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _train(pipelined, steps, n_importance=64):
+def _train(pipelined, steps, n_importance=64, flush=False):
     from nerf_pl_amd import Embedding, NeRF, render_rays
     from nerf_pl_amd.losses import MSELoss
     from nerf_pl_amd.optim import FusedAdam
@@ -38,6 +38,8 @@ def _train(pipelined, steps, n_importance=64):
         try:
             for _ in range(steps):
                 losses.append(ps(step_loss).detach())
+            if flush:
+                ps.flush()
         finally:
             ps.remove()
         assert ps.mains[0] is not ps.mains[1]
@@ -69,3 +71,40 @@ def test_pipelined_step_changes_parameters():
     init = [p.detach().clone() for m in (NeRF(), NeRF()) for p in m.parameters()]
     got, _ = _train(True, 2)
     assert any(not torch.equal(a.cuda(), b) for a, b in zip(init, got))
+
+
+def test_pipelined_step_with_rccl_reducer_matches_sequential_bitwise():
+    """the distributed path at one rank (RCCL): the coarse bucket finished on
+    the next step's stream, the fine bucket and Adam deferred to the next fine
+    pass (rendering.BEFORE_FINE) -- the same parameters as the plain step"""
+    import socket
+
+    import torch.distributed as dist
+    from nerf_pl_amd.distributed import GradAllReducer
+    from nerf_pl_amd import pipeline
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    made = []
+    orig = pipeline.PipelinedStep.__init__
+
+    def init(self, models, *a, **kw):
+        red = GradAllReducer([p for m in models for p in m.parameters()],
+                             buckets=[list(m.parameters()) for m in models], hook_launch=False)
+        made.append(red)
+        orig(self, models, *a, reducer=red, **kw)
+    try:
+        pipeline.PipelinedStep.__init__ = init
+        got, got_loss = _train(True, 5, flush=True)
+    finally:
+        pipeline.PipelinedStep.__init__ = orig
+        for r in made:
+            r.remove()
+        dist.destroy_process_group()
+    ref, ref_loss = _train(False, 5)
+    assert made and made[0].hook_launch is False
+    assert torch.equal(ref_loss, got_loss), (ref_loss, got_loss)
+    for i, (a, b) in enumerate(zip(ref, got)):
+        assert torch.equal(a, b), f"parameter {i}: max |diff| {float((a - b).abs().max()):.3g}"
