@@ -50,8 +50,11 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+# before the first HIP call (nerf_pl_amd/__init__.py: why 8 hardware queues)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
