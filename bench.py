@@ -50,8 +50,11 @@ import os
 import sys
 import time
 
-# before the first HIP call (nerf_pl_amd/__init__.py: why 8 hardware queues)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# at least 8 HIP hardware queues, before the first HIP call (the GPU boxes
+# export HIP's default of 4; nerf_pl_amd/__init__.py and DESIGN.md 15: with 4,
+# RCCL's streams and the training step's three share queues and serialise)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
