@@ -10,9 +10,12 @@ import os as _os
 # with HIP's default of 4 hardware queues per process two of them share a
 # queue and their kernels serialise (measured: the distributed path's two
 # backward chains never overlapped, 488k vs 529k rays/s at one RCCL rank;
-# DESIGN.md 15).  Takes effect when set before the process's first HIP call;
-# an explicit setting wins.
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# DESIGN.md 15).  Raised to 8 when lower (the GPU boxes export HIP's default
+# of 4 explicitly) unless NERF_PL_AMD_KEEP_HW_QUEUES=1; takes effect when set
+# before the process's first HIP call.
+if (_os.environ.get("NERF_PL_AMD_KEEP_HW_QUEUES") != "1"
+        and int(_os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8):
+    _os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 from .nerf import Embedding, NeRF  # noqa: E402
 from .rendering import render_rays, sample_pdf  # noqa: E402
