@@ -1080,9 +1080,10 @@ def main():
             "rooflines": roofs_iso or roofs,
             "rooflines_basis": ("per-kernel launch times from 10 extra steps with both passes on "
                                 "one stream (the timed region overlaps the two backward chains); "
-                                "'roofline' is the kernel with the largest launch time there: "
-                                "a forward kernel (never overlapped) is taken from the timed "
-                                "region itself, a backward kernel from this serialised pass"
+                                "'roofline' is the kernel with the largest launch time there "
+                                "(fine-pass launches): a forward kernel (the fine forward never "
+                                "overlaps other work) is taken from the timed region itself, a "
+                                "backward kernel from this serialised pass"
                                 if roofs_iso else "the timed region"),
             "rooflines_concurrent": roofs_conc if roofs_iso else None,
             "mlp_stage": stage,
