@@ -71,9 +71,11 @@ class PipelinedStep:
 
     def _accumulated(self, p):
         # runs inside autograd's AccumulateGrad node, with the current stream
-        # set to the one that produced the gradient (the coarse chain's)
+        # set to the one that produced the gradient (the coarse chain's); a
+        # parameter accumulated more than once (a model used twice) records
+        # the event again, so the last accumulation is the one waited for
         self._n += 1
-        if self._n == len(self._coarse):
+        if self._n >= len(self._coarse):
             self._ev = torch.cuda.Event()
             self._ev.record()
 
