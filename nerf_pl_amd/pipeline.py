@@ -34,6 +34,8 @@ applies a deferred update (``__call__`` returns with one pending).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .optim import FusedAdam
@@ -60,7 +62,13 @@ class PipelinedStep:
             reducer.hook_launch = False
         dev = next(models[0].parameters()).device
         self.device = dev
-        self.mains = [torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev)]
+        # NERF_PL_AMD_MAIN_PRIORITY (A/B knob, e.g. -1): both main streams
+        # created with that HIP priority instead of the caller's stream + one
+        pr = os.environ.get("NERF_PL_AMD_MAIN_PRIORITY")
+        if pr is None:
+            self.mains = [torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev)]
+        else:
+            self.mains = [torch.cuda.Stream(device=dev, priority=int(pr)) for _ in range(2)]
         self.side = rendering._side_stream(dev.index)
         self.k = 0
         self._coarse = [p for p in models[0].parameters() if p.requires_grad]
